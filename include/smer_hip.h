@@ -1,0 +1,157 @@
+/*
+ * smer_hip.h — C-ABI of the MI355X (gfx950) SMER engine, libsmer_hip.so.
+ *
+ * Plain pointers (device memory owned by the caller), explicit sizes and row
+ * strides (in ELEMENTS), a dtype code, and a hipStream_t.  Every entry
+ * returns 0 on success or a negative status; smer_last_error() holds the
+ * message.  No entry allocates device memory or synchronises the stream, so
+ * every call can be captured into a hipGraph.
+ *
+ * Each entry names the reference operation it replaces (the reference is
+ * pure Python on PyTorch ATen; file:line of the call site):
+ *
+ *   smer_gemm            nn.Linear / MHA in- and out-projections, FFN, head
+ *                        (transformer.py:389,393,459,463,467; model.py:106;
+ *                        torch/nn/functional.py:6435) and their autograd
+ *                        dgrad / wgrad (train.py:783)
+ *   smer_attn_fwd/bwd    MHA scaled-dot-product path with key-padding and
+ *                        causal masks (functional.py:6578-6600 via
+ *                        transformer.py:389,459,463) and its backward
+ *   smer_attn_weights    head-averaged cross-attention weights
+ *                        (functional.py:6606, transformer.py:332, model.py:101)
+ *   smer_attn_decode     KV-cached single-step attention for the infill loop
+ *                        (replaces the full recompute of generation.py:217)
+ *   smer_kv_scatter      append new K/V rows to a per-request cache
+ *   smer_layernorm_*     residual LayerNorm, eps 1e-5 (transformer.py:392,395,
+ *                        462,466,469; final norms 274-275, 329-330)
+ *   smer_embed_*         embedding gather x sqrt(d) + sinusoidal PE + dropout
+ *                        (model.py:91-92,124-125) and its scatter backward
+ *   smer_wce_*           the 7-12 weighted cross-entropy criteria fused into
+ *                        one pass (train.py:555-642,726-780)
+ *   smer_adam            torch.optim.Adam step (train.py:264,786)
+ *   smer_colsum          bias gradients (autograd of nn.Linear bias)
+ *   smer_cast            fp32 master -> bf16 working copies
+ */
+#ifndef SMER_HIP_H
+#define SMER_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* smer_stream_t; /* == hipStream_t */
+
+#define SMER_OK 0
+#define SMER_ERR_INVALID (-1)
+#define SMER_ERR_HIP (-2)
+#define SMER_ERR_UNSUPPORTED (-3)
+
+#define SMER_F32 0
+#define SMER_BF16 1
+
+int smer_abi_version(void);
+const char* smer_last_error(void);
+
+/* C = epilogue(alpha * op(A) op(B)^T).
+ *   a_kcontig=1: A is [M,K] row-major (lda >= K); 0: A is [K,M] (lda >= M).
+ *   b_kcontig=1: B is [N,K] row-major (ldb >= K); 0: B is [K,N] (ldb >= N).
+ * epilogue(v) = residual + dropout(relu?(v + bias))  then  *gate-mask,
+ *   gate (nullable, [M,N] ld ldg): v *= (gate > 0 ? gate_scale : 0)
+ * outputs: C (activation dtype, nullable) and/or Cf (fp32, nullable;
+ *   accumulate=1 adds into Cf).  bf16 path: MFMA 16x16x32; f32 path: VALU. */
+int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
+              const void* A, long lda, const void* B, long ldb,
+              const float* bias, float alpha, int relu,
+              const void* residual, long ldr,
+              const void* gate, long ldg, float gate_scale,
+              float drop_p, uint32_t drop_seed,
+              void* C, long ldc, float* Cf, long ldcf, int accumulate,
+              smer_stream_t stream);
+
+/* Flash attention over [B*L, *] token-row layouts (row = b*L + i), head h
+ * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:
+ * key j visible to query i iff j <= i.  lse: fp32 [B, H, Lq] (natural log).
+ * Attention-probability dropout with (drop_p, seed). */
+int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D,
+                  const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                  void* o, long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
+                  float drop_p, uint32_t seed, smer_stream_t stream);
+size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int Lk);
+int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D,
+                  const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                  const void* o, long ldo, const void* dout, long lddo, const float* lse,
+                  const uint8_t* kpm, int causal, float scale, float drop_p, uint32_t seed,
+                  void* dq, long lddq, void* dk, long lddk, void* dv, long lddv,
+                  void* workspace, size_t ws_bytes, smer_stream_t stream);
+/* out fp32 [B, Lq, Lk] = mean over heads of the attention probabilities. */
+int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
+                      const void* q, long ldq, const void* k, long ldk, const float* lse,
+                      const uint8_t* kpm, int causal, float scale, float* out,
+                      smer_stream_t stream);
+/* Decode attention: row r (query q[r], head h at column h*D) attends keys
+ * 0..row_nkeys[r]-1 of request row_req[r] in caches laid out
+ * cache[req * req_stride + j * row_stride + h*D + d]. */
+int smer_attn_decode(int dtype, int n_rows, int H, int D, const void* q, long ldq,
+                     const void* kcache, const void* vcache, long row_stride, long req_stride,
+                     const int32_t* row_req, const int32_t* row_nkeys, void* o, long ldo,
+                     float scale, smer_stream_t stream);
+int smer_kv_scatter(int dtype, int n_rows, int width, const void* src, long lds,
+                    void* cache, long row_stride, long req_stride,
+                    const int32_t* row_req, const int32_t* row_pos, smer_stream_t stream);
+
+int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long ldx,
+                       const float* gamma, const float* beta, float eps,
+                       void* y, long ldy, float* mean, float* rstd, smer_stream_t stream);
+size_t smer_layernorm_bwd_workspace(int M, int N);
+/* dx = dLN/d(input); optional dx_drop = dx * keep(seed,row,col)/(1-p).
+ * dy_f32=1: dy is fp32 (else activation dtype).  dgamma/dbeta (fp32,
+ * nullable) receive (accumulate=1: +=) the column sums. */
+int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
+                       const void* x, long ldx, const float* mean, const float* rstd,
+                       const float* gamma, void* dx, long lddx,
+                       void* dx_drop, long ldxd, float drop_p, uint32_t seed,
+                       float* dgamma, float* dbeta, int accumulate,
+                       void* workspace, size_t ws_bytes, smer_stream_t stream);
+
+/* out[t] = dropout(table[ids[t]] * scale + pe[pos(t)]), pos(t) = positions
+ * ? positions[t] : t % L.  table/pe fp32; out activation dtype. */
+int smer_embed_fwd(int dtype, int n_tok, int d, const int64_t* ids, const int32_t* positions,
+                   int L, const float* table, const float* pe, float scale,
+                   float drop_p, uint32_t seed, void* out, long ldo, smer_stream_t stream);
+size_t smer_embed_bwd_workspace(int V, int d, int n_tok_total);
+/* dtable[v] += scale * sum over both segments of dx[t] * keep/(1-p). */
+int smer_embed_bwd(int dtype, int V, int d, float scale,
+                   const int64_t* ids0, const void* dx0, long ld0, int n0, float p0, uint32_t seed0,
+                   const int64_t* ids1, const void* dx1, long ld1, int n1, float p1, uint32_t seed1,
+                   float* dtable, void* workspace, size_t ws_bytes, smer_stream_t stream);
+
+/* denom = sum_i ce_all[y_i] (train.py:736-742). */
+int smer_wce_denom(int n, const int64_t* y, const float* ce_all, float* denom,
+                   smer_stream_t stream);
+/* Per row r: l_r = w[y_r] * (logsumexp(x_r) - x_r[y_r]) (0 for y_r == 0);
+ * dlogits_r = grad_scale * w[y_r]/denom * (softmax(x_r) - onehot(y_r)).
+ * loss = sum_r l_r / denom written to loss_out (fp32 scalar).  dlog dtype. */
+int smer_wce_fwd_bwd(int dtype, int R, int V, const float* logits, long ldl, const int64_t* y,
+                     const float* w, const float* denom, float* row_loss, float* loss_out,
+                     void* dlogits, long ldd, float grad_scale, smer_stream_t stream);
+
+/* torch.optim.Adam step on flat fp32 buffers; p_bf16 (nullable) receives
+ * the bf16 working copy.  bc1 = 1-b1^t, bc2_sqrt = sqrt(1-b2^t). */
+int smer_adam(long n, float* p, const float* g, float* m, float* v, void* p_bf16,
+              float lr, float b1, float b2, float eps, float bc1, float bc2_sqrt,
+              smer_stream_t stream);
+
+int smer_cast(int src_dtype, int dst_dtype, long n, const void* src, void* dst,
+              smer_stream_t stream);
+size_t smer_colsum_workspace(int M, int N);
+/* out[n] (+)= sum_m x[m, n] (deterministic two-stage). */
+int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, int accumulate,
+                void* workspace, size_t ws_bytes, smer_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMER_HIP_H */

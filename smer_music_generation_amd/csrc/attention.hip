@@ -1,0 +1,862 @@
+// Attention kernels: the MHA math path of the reference
+// (torch/nn/functional.py:6578-6600 via transformer.py:389,459,463).
+//
+// bf16 flash forward / backward (gfx950 MFMA 16x16x32):
+//  * "key on the row" orientation: S^T = K Q^T, so each lane holds one query
+//    column and its softmax row lives in 16 registers + 2 cross-group
+//    shuffles; P feeds the P.V MFMA as the B operand straight from registers
+//    (the k order of the 32-key step is permuted identically on both
+//    operands), V is consumed through ds_read_b64_tr_b16.
+//  * backward = dK/dV pass (one workgroup per 64 keys, loops over queries)
+//    + dQ pass (one workgroup per 64 queries, loops over keys): no atomics,
+//    deterministic.
+// f32 kernels (parity mode) are plain row-per-wave VALU kernels.
+#include "common.h"
+
+#define LOG2E_F 1.4426950408889634f
+#define LN2_F 0.6931471805599453f
+
+namespace {
+constexpr int KVB = 64;  // keys (or queries) per LDS tile
+
+template <int D>
+struct AttnCfg {
+  static constexpr int ROWB = D * 2 + 16;            // padded LDS row bytes
+  static constexpr int NS = D / 32;                  // 32-deep k-steps over the head dim
+  static constexpr int NDT = D / 16;                 // 16-wide head-dim tiles
+  static constexpr int CPR = D / 8;                  // 16-B chunks per row
+  static constexpr int CPT = (KVB * CPR) / 256;      // chunks per thread per tile
+  static constexpr int TILE = KVB * ROWB;
+};
+
+template <int D>
+__device__ __forceinline__ void tile_load(uint4 (&r)[AttnCfg<D>::CPT], const bf16* base, long ld,
+                                          int row0, int nrows, int tid) {
+#pragma unroll
+  for (int c = 0; c < AttnCfg<D>::CPT; ++c) {
+    int i = tid + 256 * c;
+    int row = i / AttnCfg<D>::CPR, ch = i % AttnCfg<D>::CPR;
+    int gr = row0 + row;
+    r[c] = gr < nrows ? *reinterpret_cast<const uint4*>(base + (long)gr * ld + ch * 8)
+                      : make_uint4(0, 0, 0, 0);
+  }
+}
+template <int D>
+__device__ __forceinline__ void tile_store(const uint4 (&r)[AttnCfg<D>::CPT], char* buf, int tid) {
+#pragma unroll
+  for (int c = 0; c < AttnCfg<D>::CPT; ++c) {
+    int i = tid + 256 * c;
+    int row = i / AttnCfg<D>::CPR, ch = i % AttnCfg<D>::CPR;
+    *reinterpret_cast<uint4*>(buf + row * AttnCfg<D>::ROWB + ch * 16) = r[c];
+  }
+}
+// Row fragment: rows rbase+c16, head-dim k-step s (8 contiguous elements).
+template <int D>
+__device__ __forceinline__ bf16x8 row_frag(const char* buf, int rbase, int s, int lane) {
+  return lds_read_b128(buf, (rbase + (lane & 15)) * AttnCfg<D>::ROWB + (s * 32 + 8 * (lane >> 4)) * 2);
+}
+// Transposed fragment for the 32-row step ks over head-dim tile dt: element
+// j of lane-group g = row ks*32 + (j<4 ? 4g+j : 16+4g+j-4), column dt*16+c16.
+template <int D>
+__device__ __forceinline__ bf16x8 tr_frag(const char* buf, int ks, int dt, int lane) {
+  int g = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
+  int col = (dt * 16 + 4 * pp) * 2;
+  bf16x4 lo = lds_read_tr16(buf, (ks * 32 + 4 * g + qq) * AttnCfg<D>::ROWB + col);
+  bf16x4 hi = lds_read_tr16(buf, (ks * 32 + 16 + 4 * g + qq) * AttnCfg<D>::ROWB + col);
+  return cat4(lo, hi);
+}
+__device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (bf16)p[2 * ks][j];
+    r[4 + j] = (bf16)p[2 * ks + 1][j];
+  }
+  return r;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// bf16 forward
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
+                                                     const bf16* __restrict__ q, long ldq,
+                                                     const bf16* __restrict__ k, long ldk,
+                                                     const bf16* __restrict__ v, long ldv,
+                                                     bf16* __restrict__ o, long ldo,
+                                                     float* __restrict__ lse,
+                                                     const uint8_t* __restrict__ kpm, int causal,
+                                                     float scale, uint32_t drop_thr, uint32_t seed,
+                                                     float drop_scale) {
+  using C = AttnCfg<D>;
+  __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int qi = blockIdx.x * 64 + wave * 16 + c16;
+  const bool qvalid = qi < Lq;
+  const float c = scale * LOG2E_F;
+
+  bf16x8 qf[C::NS];
+  {
+    const bf16* qrow = q + (long)(b * Lq + min(qi, Lq - 1)) * ldq + h * D;
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qrow + s * 32 + 8 * g);
+      if (!qvalid) qf[s] = bf16x8{};
+    }
+  }
+  const bf16* kb = k + (long)b * Lk * ldk + h * D;
+  const bf16* vb = v + (long)b * Lk * ldv + h * D;
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+
+  int n_tiles = (Lk + KVB - 1) / KVB;
+  if (causal) {
+    int qmax = min(Lq, (int)blockIdx.x * 64 + 64);
+    n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
+  }
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 acc[C::NDT];
+#pragma unroll
+  for (int i = 0; i < C::NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 rk[C::CPT], rv[C::CPT];
+  if (n_tiles > 0) {
+    tile_load<D>(rk, kb, ldk, 0, Lk, tid);
+    tile_load<D>(rv, vb, ldv, 0, Lk, tid);
+    tile_store<D>(rk, sm[0][0], tid);
+    tile_store<D>(rv, sm[0][1], tid);
+  }
+  __syncthreads();
+  const uint32_t qrow_id = (uint32_t)(bh * Lq + qi);
+  for (int t = 0; t < n_tiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < n_tiles;
+    if (more) {
+      tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
+      tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
+    }
+    const char* Ks = sm[cur][0];
+    const char* Vs = sm[cur][1];
+    f32x4 st[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      st[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::NS; ++s) st[mt] = mfma16(row_frag<D>(Ks, mt * 16, s, lane), qf[s], st[mt]);
+    }
+    float x[4][4];
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int key = t * KVB + mt * 16 + 4 * g + r;
+        bool ok = key < Lk && (!kp || !kp[key]) && (!causal || key <= qi);
+        float xv = ok ? st[mt][r] * c : -INFINITY;
+        x[mt][r] = xv;
+        tmax = fmaxf(tmax, xv);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    l_run *= alpha;
+#pragma unroll
+    for (int i = 0; i < C::NDT; ++i) acc[i] *= alpha;
+    float p[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = exp2f(x[mt][r] - m_use);
+        l_run += pv;
+        if (drop_thr) {
+          int key = t * KVB + mt * 16 + 4 * g + r;
+          pv = smer_keep(seed, drop_thr, qrow_id, (uint32_t)key) ? pv * drop_scale : 0.f;
+        }
+        p[mt][r] = pv;
+      }
+    m_run = m_new;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pf = pack_p(p, ks);
+#pragma unroll
+      for (int dt = 0; dt < C::NDT; ++dt) acc[dt] = mfma16(tr_frag<D>(Vs, ks, dt, lane), pf, acc[dt]);
+    }
+    if (more) {
+      tile_store<D>(rk, sm[cur ^ 1][0], tid);
+      tile_store<D>(rv, sm[cur ^ 1][1], tid);
+    }
+    __syncthreads();
+  }
+  float l = l_run + __shfl_xor(l_run, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qvalid) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  bf16* orow = o + (long)(b * Lq + qi) * ldo + h * D;
+#pragma unroll
+  for (int dt = 0; dt < C::NDT; ++dt) {
+    bf16x4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[dt][r] * inv);
+    *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
+  }
+  if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_run + log2f(l)) * LN2_F : INFINITY;
+}
+
+// ---------------------------------------------------------------------------
+// bf16 backward: dK / dV
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
+    int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
+    const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
+    const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
+    const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
+    uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dk, long lddk,
+    bf16* __restrict__ dv, long lddv) {
+  using C = AttnCfg<D>;
+  __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
+  __shared__ float s_lse[2][KVB], s_del[2][KVB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int kj = blockIdx.x * 64 + wave * 16 + c16;
+  const bool kvalid = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
+  const float c = scale * LOG2E_F;
+
+  bf16x8 kf[C::NS], vf[C::NS];
+  {
+    long row = (long)(b * Lk + min(kj, Lk - 1));
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(k + row * ldk + h * D + s * 32 + 8 * g);
+      vf[s] = *reinterpret_cast<const bf16x8*>(v + row * ldv + h * D + s * 32 + 8 * g);
+      if (kj >= Lk) { kf[s] = bf16x8{}; vf[s] = bf16x8{}; }
+    }
+  }
+  const bf16* qb = q + (long)b * Lq * ldq + h * D;
+  const bf16* ob = dout + (long)b * Lq * lddo + h * D;
+  const float* lb = lse + (long)bh * Lq;
+  const float* db = delta + (long)bh * Lq;
+
+  const int n_qt = (Lq + KVB - 1) / KVB;
+  const int t0 = causal ? min(n_qt, (int)(blockIdx.x * 64) / KVB) : 0;
+  f32x4 adk[C::NDT], adv[C::NDT];
+#pragma unroll
+  for (int i = 0; i < C::NDT; ++i) { adk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; adv[i] = adk[i]; }
+
+  uint4 rq[C::CPT], ro[C::CPT];
+  float rl = 0.f, rd = 0.f;
+  auto load = [&](int t) {
+    tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
+    tile_load<D>(ro, ob, lddo, t * KVB, Lq, tid);
+    if (tid < KVB) {
+      int qq = t * KVB + tid;
+      rl = qq < Lq ? lb[qq] * LOG2E_F : INFINITY;
+      rd = qq < Lq ? db[qq] : 0.f;
+    }
+  };
+  auto store = [&](int buf) {
+    tile_store<D>(rq, sm[buf][0], tid);
+    tile_store<D>(ro, sm[buf][1], tid);
+    if (tid < KVB) { s_lse[buf][tid] = rl; s_del[buf][tid] = rd; }
+  };
+  if (t0 < n_qt) { load(t0); store(0); }
+  __syncthreads();
+  for (int t = t0; t < n_qt; ++t) {
+    const int cur = (t - t0) & 1;
+    const bool more = t + 1 < n_qt;
+    if (more) load(t + 1);
+    const char* Qs = sm[cur][0];
+    const char* Os = sm[cur][1];
+    float pd[4][4], ds[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
+#pragma unroll
+      for (int s = 0; s < C::NS; ++s) {
+        sacc = mfma16(row_frag<D>(Qs, mt * 16, s, lane), kf[s], sacc);
+        dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[s], dpacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int ql = mt * 16 + 4 * g + r;
+        int qq = t * KVB + ql;
+        bool ok = qq < Lq && kvalid && (!causal || kj <= qq);
+        float pv = ok ? exp2f(sacc[r] * c - s_lse[cur][ql]) : 0.f;
+        float dpv = dpacc[r];
+        float pdv = pv;
+        if (drop_thr) {
+          bool keep = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qq), (uint32_t)kj);
+          pdv = keep ? pv * drop_scale : 0.f;
+          dpv = keep ? dpv * drop_scale : 0.f;
+        }
+        pd[mt][r] = pdv;
+        ds[mt][r] = pv * (dpv - s_del[cur][ql]);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 pf = pack_p(pd, ks);
+      bf16x8 sf = pack_p(ds, ks);
+#pragma unroll
+      for (int dt = 0; dt < C::NDT; ++dt) {
+        adv[dt] = mfma16(tr_frag<D>(Os, ks, dt, lane), pf, adv[dt]);
+        adk[dt] = mfma16(tr_frag<D>(Qs, ks, dt, lane), sf, adk[dt]);
+      }
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+  if (kj >= Lk) return;
+  bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
+  bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
+#pragma unroll
+  for (int dt = 0; dt < C::NDT; ++dt) {
+    bf16x4 wk, wv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(adk[dt][r] * scale); wv[r] = (bf16)adv[dt][r]; }
+    *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
+    *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 backward: dQ
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
+    int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
+    const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
+    const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
+    const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
+    uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq) {
+  using C = AttnCfg<D>;
+  __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int qi = blockIdx.x * 64 + wave * 16 + c16;
+  const bool qvalid = qi < Lq;
+  const float c = scale * LOG2E_F;
+  bf16x8 qf[C::NS], of[C::NS];
+  {
+    long row = (long)(b * Lq + min(qi, Lq - 1));
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
+      of[s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
+      if (!qvalid) { qf[s] = bf16x8{}; of[s] = bf16x8{}; }
+    }
+  }
+  const float lse2 = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
+  const float dlt = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
+  const bf16* kb = k + (long)b * Lk * ldk + h * D;
+  const bf16* vb = v + (long)b * Lk * ldv + h * D;
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  int n_tiles = (Lk + KVB - 1) / KVB;
+  if (causal) {
+    int qmax = min(Lq, (int)blockIdx.x * 64 + 64);
+    n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
+  }
+  f32x4 adq[C::NDT];
+#pragma unroll
+  for (int i = 0; i < C::NDT; ++i) adq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 rk[C::CPT], rv[C::CPT];
+  if (n_tiles > 0) {
+    tile_load<D>(rk, kb, ldk, 0, Lk, tid);
+    tile_load<D>(rv, vb, ldv, 0, Lk, tid);
+    tile_store<D>(rk, sm[0][0], tid);
+    tile_store<D>(rv, sm[0][1], tid);
+  }
+  __syncthreads();
+  const uint32_t qrow_id = (uint32_t)(bh * Lq + qi);
+  for (int t = 0; t < n_tiles; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < n_tiles;
+    if (more) {
+      tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
+      tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
+    }
+    const char* Ks = sm[cur][0];
+    const char* Vs = sm[cur][1];
+    float ds[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
+#pragma unroll
+      for (int s = 0; s < C::NS; ++s) {
+        sacc = mfma16(row_frag<D>(Ks, mt * 16, s, lane), qf[s], sacc);
+        dpacc = mfma16(row_frag<D>(Vs, mt * 16, s, lane), of[s], dpacc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int key = t * KVB + mt * 16 + 4 * g + r;
+        bool ok = qvalid && key < Lk && (!kp || !kp[key]) && (!causal || key <= qi);
+        float pv = ok ? exp2f(sacc[r] * c - lse2) : 0.f;
+        float dpv = dpacc[r];
+        if (drop_thr)
+          dpv = smer_keep(seed, drop_thr, qrow_id, (uint32_t)key) ? dpv * drop_scale : 0.f;
+        ds[mt][r] = pv * (dpv - dlt);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 sf = pack_p(ds, ks);
+#pragma unroll
+      for (int dt = 0; dt < C::NDT; ++dt) adq[dt] = mfma16(tr_frag<D>(Ks, ks, dt, lane), sf, adq[dt]);
+    }
+    if (more) {
+      tile_store<D>(rk, sm[cur ^ 1][0], tid);
+      tile_store<D>(rv, sm[cur ^ 1][1], tid);
+    }
+    __syncthreads();
+  }
+  if (!qvalid) return;
+  bf16* dqr = dq + (long)(b * Lq + qi) * lddq + h * D;
+#pragma unroll
+  for (int dt = 0; dt < C::NDT; ++dt) {
+    bf16x4 w;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) w[r] = (bf16)(adq[dt][r] * scale);
+    *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;
+  }
+}
+
+// delta[bh, i] = sum_d dO[i, h*D + d] * O[i, h*D + d]
+template <typename T>
+__global__ void attn_delta(int B, int H, int Lq, int D, const T* __restrict__ o, long ldo,
+                           const T* __restrict__ dout, long lddo, float* __restrict__ delta) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * H * Lq;
+  if (idx >= total) return;
+  int i = idx % Lq;
+  int bh = idx / Lq;
+  int b = bh / H, h = bh % H;
+  const T* orow = o + (long)(b * Lq + i) * ldo + h * D;
+  const T* drow = dout + (long)(b * Lq + i) * lddo + h * D;
+  float s = 0.f;
+  for (int d = 0; d < D; ++d) s += to_f32(orow[d]) * to_f32(drow[d]);
+  delta[idx] = s;
+}
+
+// ---------------------------------------------------------------------------
+// f32 kernels (parity mode): one wave per query row
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool attn_visible(const uint8_t* kp, int key, int qi, int causal) {
+  return (!kp || !kp[key]) && (!causal || key <= qi);
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_f32(int B, int H, int Lq, int Lk, int D,
+                                                    const float* __restrict__ q, long ldq,
+                                                    const float* __restrict__ k, long ldk,
+                                                    const float* __restrict__ v, long ldv,
+                                                    float* __restrict__ o, long ldo,
+                                                    float* __restrict__ lse,
+                                                    const uint8_t* __restrict__ kpm, int causal,
+                                                    float scale, uint32_t drop_thr, uint32_t seed,
+                                                    float drop_scale) {
+  extern __shared__ float sc_all[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int qi = blockIdx.x * 4 + wave;
+  if (qi >= Lq) return;
+  float* sc = sc_all + wave * Lk;
+  const float* qrow = q + (long)(b * Lq + qi) * ldq + h * D;
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  float mx = -INFINITY;
+  for (int j = lane; j < Lk; j += 64) {
+    float s = -INFINITY;
+    if (attn_visible(kp, j, qi, causal)) {
+      const float* krow = k + (long)(b * Lk + j) * ldk + h * D;
+      float a = 0.f;
+      for (int d = 0; d < D; ++d) a = fmaf(qrow[d] * scale, krow[d], a);
+      s = a;
+    }
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  const float mu = mx == -INFINITY ? 0.f : mx;
+  float sum = 0.f;
+  for (int j = lane; j < Lk; j += 64) {
+    float e = expf(sc[j] - mu);
+    sum += e;
+    if (drop_thr) e = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qi), (uint32_t)j) ? e * drop_scale : 0.f;
+    sc[j] = e;
+  }
+  sum = wave_sum(sum);
+  __builtin_amdgcn_wave_barrier();
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+  for (int d = lane; d < D; d += 64) {
+    float a = 0.f;
+    for (int j = 0; j < Lk; ++j) a = fmaf(sc[j], v[(long)(b * Lk + j) * ldv + h * D + d], a);
+    o[(long)(b * Lq + qi) * ldo + h * D + d] = a * inv;
+  }
+  if (lane == 0) lse[(long)bh * Lq + qi] = sum > 0.f ? mu + logf(sum) : INFINITY;
+}
+
+// P / dS materialisation: ws_p = dropped P, ws_s = dS  ([B*H, Lq, Lk])
+__global__ void attn_bwd_ps_f32(int B, int H, int Lq, int Lk, int D, const float* q, long ldq,
+                                const float* k, long ldk, const float* v, long ldv,
+                                const float* dout, long lddo, const float* lse,
+                                const float* delta, const uint8_t* kpm, int causal, float scale,
+                                uint32_t drop_thr, uint32_t seed, float drop_scale, float* ws_p,
+                                float* ws_s) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * H * Lq * Lk;
+  if (idx >= total) return;
+  int j = idx % Lk;
+  long r = idx / Lk;
+  int qi = r % Lq;
+  int bh = r / Lq, b = bh / H, h = bh % H;
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  float p = 0.f, dp = 0.f;
+  if (attn_visible(kp, j, qi, causal)) {
+    const float* qrow = q + (long)(b * Lq + qi) * ldq + h * D;
+    const float* krow = k + (long)(b * Lk + j) * ldk + h * D;
+    const float* vrow = v + (long)(b * Lk + j) * ldv + h * D;
+    const float* orow = dout + (long)(b * Lq + qi) * lddo + h * D;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) { s = fmaf(qrow[d] * scale, krow[d], s); dp = fmaf(orow[d], vrow[d], dp); }
+    p = expf(s - lse[r]);
+  }
+  float pd = p;
+  if (drop_thr) {
+    bool keep = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qi), (uint32_t)j);
+    pd = keep ? p * drop_scale : 0.f;
+    dp = keep ? dp * drop_scale : 0.f;
+  }
+  ws_p[idx] = pd;
+  ws_s[idx] = p * (dp - delta[r]);
+}
+
+// dK, dV rows: thread per (bh, key, d)
+__global__ void attn_bwd_kv_f32(int B, int H, int Lq, int Lk, int D, const float* q, long ldq,
+                                const float* dout, long lddo, const float* ws_p,
+                                const float* ws_s, float scale, float* dk, long lddk, float* dv,
+                                long lddv) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * H * Lk * D;
+  if (idx >= total) return;
+  int d = idx % D;
+  long r = idx / D;
+  int j = r % Lk;
+  int bh = r / Lk, b = bh / H, h = bh % H;
+  float ak = 0.f, av = 0.f;
+  const float* P = ws_p + (long)bh * Lq * Lk + j;
+  const float* S = ws_s + (long)bh * Lq * Lk + j;
+  for (int i = 0; i < Lq; ++i) {
+    long row = (long)(b * Lq + i);
+    ak = fmaf(S[(long)i * Lk], q[row * ldq + h * D + d], ak);
+    av = fmaf(P[(long)i * Lk], dout[row * lddo + h * D + d], av);
+  }
+  dk[(long)(b * Lk + j) * lddk + h * D + d] = ak * scale;
+  dv[(long)(b * Lk + j) * lddv + h * D + d] = av;
+}
+
+__global__ void attn_bwd_q_f32(int B, int H, int Lq, int Lk, int D, const float* k, long ldk,
+                               const float* ws_s, float scale, float* dq, long lddq) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * H * Lq * D;
+  if (idx >= total) return;
+  int d = idx % D;
+  long r = idx / D;
+  int qi = r % Lq;
+  int bh = r / Lq, b = bh / H, h = bh % H;
+  const float* S = ws_s + ((long)bh * Lq + qi) * Lk;
+  float a = 0.f;
+  for (int j = 0; j < Lk; ++j) a = fmaf(S[j], k[(long)(b * Lk + j) * ldk + h * D + d], a);
+  dq[(long)(b * Lq + qi) * lddq + h * D + d] = a * scale;
+}
+
+// head-averaged probabilities (the `weights` the reference returns)
+template <typename T>
+__global__ void attn_weights_kernel(int B, int H, int Lq, int Lk, int D, const T* q, long ldq,
+                                    const T* k, long ldk, const float* lse, const uint8_t* kpm,
+                                    int causal, float scale, float* out) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * Lq * Lk;
+  if (idx >= total) return;
+  int j = idx % Lk;
+  long r = idx / Lk;
+  int qi = r % Lq;
+  int b = r / Lq;
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  float acc = 0.f;
+  if (attn_visible(kp, j, qi, causal)) {
+    for (int h = 0; h < H; ++h) {
+      const T* qrow = q + (long)(b * Lq + qi) * ldq + h * D;
+      const T* krow = k + (long)(b * Lk + j) * ldk + h * D;
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) s = fmaf(to_f32(qrow[d]), to_f32(krow[d]), s);
+      acc += expf(s * scale - lse[((long)b * H + h) * Lq + qi]);
+    }
+  }
+  out[idx] = acc / H;
+}
+
+// ---------------------------------------------------------------------------
+// decode attention (KV cache) — one workgroup per (row, head)
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void attn_decode_kernel(int H, int D, const T* __restrict__ q,
+                                                          long ldq, const T* __restrict__ kc,
+                                                          const T* __restrict__ vc,
+                                                          long row_stride, long req_stride,
+                                                          const int32_t* __restrict__ row_req,
+                                                          const int32_t* __restrict__ row_nkeys,
+                                                          T* __restrict__ o, long ldo,
+                                                          float scale) {
+  extern __shared__ float dsm[];
+  __shared__ float red[8];
+  __shared__ float qs[256];
+  __shared__ float part[4][256];
+  const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int nk = row_nkeys[r];
+  const long base = (long)row_req[r] * req_stride + h * D;
+  for (int d = tid; d < D; d += 256) qs[d] = to_f32(q[(long)r * ldq + h * D + d]) * scale;
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = tid; j < nk; j += 256) {
+    const T* kr = kc + base + (long)j * row_stride;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s = fmaf(qs[d], to_f32(kr[d]), s);
+    dsm[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = tid; j < nk; j += 256) {
+    float e = expf(dsm[j] - mx);
+    dsm[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+  __syncthreads();
+  sum = red[4] + red[5] + red[6] + red[7];
+  // 4 key groups x 64 lanes over d
+  const int grp = tid >> 6, ln = tid & 63;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    int d = d0 + ln;
+    float a = 0.f;
+    if (d < D)
+      for (int j = grp; j < nk; j += 4) a = fmaf(dsm[j], to_f32(vc[base + (long)j * row_stride + d]), a);
+    part[grp][ln] = a;
+    __syncthreads();
+    if (grp == 0 && d < D) {
+      float t = (part[0][ln] + part[1][ln]) + (part[2][ln] + part[3][ln]);
+      o[(long)r * ldo + h * D + d] = from_f32<T>(sum > 0.f ? t / sum : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ void kv_scatter_kernel(int n_rows, int width, const T* __restrict__ src, long lds,
+                                  T* __restrict__ cache, long row_stride, long req_stride,
+                                  const int32_t* __restrict__ row_req,
+                                  const int32_t* __restrict__ row_pos) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)n_rows * width) return;
+  int r = idx / width, c = idx % width;
+  cache[(long)row_req[r] * req_stride + (long)row_pos[r] * row_stride + c] = src[(long)r * lds + c];
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int D>
+static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
+                            long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
+                            const uint8_t* kpm, int causal, float scale, uint32_t thr,
+                            uint32_t seed, float ds, hipStream_t s) {
+  dim3 grid((Lq + 63) / 64, B * H);
+  hipLaunchKernelGGL(attn_fwd_bf16<D>, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
+                     (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
+                     scale, thr, seed, ds);
+}
+
+extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                             long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
+                             long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
+                             float drop_p, uint32_t seed, smer_stream_t stream) {
+  SMER_REQUIRE(B > 0 && H > 0 && Lq >= 0 && Lk > 0 && D > 0, "smer_attn_fwd: bad sizes");
+  SMER_REQUIRE(q && k && v && o && lse, "smer_attn_fwd: null pointer");
+  SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
+  if (Lq == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t thr = smer_drop_threshold(drop_p);
+  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  if (dtype == SMER_BF16) {
+    SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
+    SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
+                 "smer_attn_fwd: row strides must be multiples of 8");
+    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
+    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
+    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
+    else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd(bf16): head dim must be 32, 64 or 128");
+  } else if (dtype == SMER_F32) {
+    SMER_REQUIRE((size_t)Lk * 16 <= 160 * 1024, "smer_attn_fwd(f32): Lk too large");
+    dim3 grid((Lq + 3) / 4, B * H);
+    hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(256), (size_t)Lk * 16, s, B, H, Lq, Lk, D,
+                       (const float*)q, ldq, (const float*)k, ldk, (const float*)v, ldv,
+                       (float*)o, ldo, lse, kpm, causal, scale, thr, seed, ds);
+  } else {
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd: dtype");
+  }
+  SMER_CHECK_LAUNCH("smer_attn_fwd");
+  return SMER_OK;
+}
+
+extern "C" size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int Lk) {
+  size_t delta = ((size_t)B * H * Lq * sizeof(float) + 255) & ~(size_t)255;
+  if (dtype == SMER_F32) return delta + 2 * (size_t)B * H * Lq * Lk * sizeof(float);
+  return delta;
+}
+
+template <int D>
+static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
+                            long ldk, const void* v, long ldv, const void* dout, long lddo,
+                            const float* lse, const float* delta, const uint8_t* kpm, int causal,
+                            float scale, uint32_t thr, uint32_t seed, float ds, void* dq,
+                            long lddq, void* dk, long lddk, void* dv, long lddv, hipStream_t s) {
+  hipLaunchKernelGGL(attn_bwd_dkdv_bf16<D>, dim3((Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+                     Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
+                     (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
+                     (bf16*)dk, lddk, (bf16*)dv, lddv);
+  hipLaunchKernelGGL(attn_bwd_dq_bf16<D>, dim3((Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+                     Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
+                     (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
+                     (bf16*)dq, lddq);
+}
+
+extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                             long ldq, const void* k, long ldk, const void* v, long ldv,
+                             const void* o, long ldo, const void* dout, long lddo,
+                             const float* lse, const uint8_t* kpm, int causal, float scale,
+                             float drop_p, uint32_t seed, void* dq, long lddq, void* dk, long lddk,
+                             void* dv, long lddv, void* workspace, size_t ws_bytes,
+                             smer_stream_t stream) {
+  SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && D > 0, "smer_attn_bwd: bad sizes");
+  SMER_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "smer_attn_bwd: null pointer");
+  SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
+               "smer_attn_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  uint32_t thr = smer_drop_threshold(drop_p);
+  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  float* delta = (float*)workspace;
+  long nrow = (long)B * H * Lq;
+  if (dtype == SMER_BF16) {
+    SMER_REQUIRE(al16(q) && al16(k) && al16(v) && al16(dout), "smer_attn_bwd: 16-B alignment");
+    hipLaunchKernelGGL(attn_delta<bf16>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H, Lq, D,
+                       (const bf16*)o, ldo, (const bf16*)dout, lddo, delta);
+    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
+    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
+    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
+    else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd(bf16): head dim must be 32, 64 or 128");
+  } else if (dtype == SMER_F32) {
+    hipLaunchKernelGGL(attn_delta<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H, Lq, D,
+                       (const float*)o, ldo, (const float*)dout, lddo, delta);
+    size_t doff = ((size_t)nrow * sizeof(float) + 255) & ~(size_t)255;
+    float* ws_p = (float*)((char*)workspace + doff);
+    float* ws_s = ws_p + (size_t)B * H * Lq * Lk;
+    long tot = (long)B * H * Lq * Lk;
+    hipLaunchKernelGGL(attn_bwd_ps_f32, dim3((tot + 255) / 256), dim3(256), 0, s, B, H, Lq, Lk, D,
+                       (const float*)q, ldq, (const float*)k, ldk, (const float*)v, ldv,
+                       (const float*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
+                       ws_p, ws_s);
+    long tk = (long)B * H * Lk * D;
+    hipLaunchKernelGGL(attn_bwd_kv_f32, dim3((tk + 255) / 256), dim3(256), 0, s, B, H, Lq, Lk, D,
+                       (const float*)q, ldq, (const float*)dout, lddo, ws_p, ws_s, scale,
+                       (float*)dk, lddk, (float*)dv, lddv);
+    long tq = (long)B * H * Lq * D;
+    hipLaunchKernelGGL(attn_bwd_q_f32, dim3((tq + 255) / 256), dim3(256), 0, s, B, H, Lq, Lk, D,
+                       (const float*)k, ldk, ws_s, scale, (float*)dq, lddq);
+  } else {
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd: dtype");
+  }
+  SMER_CHECK_LAUNCH("smer_attn_bwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                                 long ldq, const void* k, long ldk, const float* lse,
+                                 const uint8_t* kpm, int causal, float scale, float* out,
+                                 smer_stream_t stream) {
+  SMER_REQUIRE(q && k && lse && out, "smer_attn_weights: null pointer");
+  long tot = (long)B * Lq * Lk;
+  if (tot == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(attn_weights_kernel<bf16>, dim3((tot + 255) / 256), dim3(256), 0, s, B, H,
+                       Lq, Lk, D, (const bf16*)q, ldq, (const bf16*)k, ldk, lse, kpm, causal,
+                       scale, out);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(attn_weights_kernel<float>, dim3((tot + 255) / 256), dim3(256), 0, s, B,
+                       H, Lq, Lk, D, (const float*)q, ldq, (const float*)k, ldk, lse, kpm, causal,
+                       scale, out);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_weights: dtype");
+  SMER_CHECK_LAUNCH("smer_attn_weights");
+  return SMER_OK;
+}
+
+extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void* q, long ldq,
+                                const void* kcache, const void* vcache, long row_stride,
+                                long req_stride, const int32_t* row_req,
+                                const int32_t* row_nkeys, void* o, long ldo, float scale,
+                                smer_stream_t stream) {
+  SMER_REQUIRE(D <= 256, "smer_attn_decode: head dim <= 256");
+  if (n_rows == 0) return SMER_OK;
+  // key capacity bounded by req_stride / row_stride rows
+  long cap = req_stride / (row_stride > 0 ? row_stride : 1);
+  SMER_REQUIRE(cap > 0 && cap * 4 <= 150 * 1024, "smer_attn_decode: cache capacity too large");
+  hipStream_t s = (hipStream_t)stream;
+  size_t shm = (size_t)cap * sizeof(float);
+  dim3 grid(n_rows, H);
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(attn_decode_kernel<bf16>, grid, dim3(256), shm, s, H, D, (const bf16*)q, ldq,
+                       (const bf16*)kcache, (const bf16*)vcache, row_stride, req_stride, row_req,
+                       row_nkeys, (bf16*)o, ldo, scale);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(attn_decode_kernel<float>, grid, dim3(256), shm, s, H, D, (const float*)q,
+                       ldq, (const float*)kcache, (const float*)vcache, row_stride, req_stride,
+                       row_req, row_nkeys, (float*)o, ldo, scale);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_decode: dtype");
+  SMER_CHECK_LAUNCH("smer_attn_decode");
+  return SMER_OK;
+}
+
+extern "C" int smer_kv_scatter(int dtype, int n_rows, int width, const void* src, long lds,
+                               void* cache, long row_stride, long req_stride,
+                               const int32_t* row_req, const int32_t* row_pos,
+                               smer_stream_t stream) {
+  long tot = (long)n_rows * width;
+  if (tot == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(kv_scatter_kernel<bf16>, dim3((tot + 255) / 256), dim3(256), 0, s, n_rows,
+                       width, (const bf16*)src, lds, (bf16*)cache, row_stride, req_stride, row_req,
+                       row_pos);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(kv_scatter_kernel<float>, dim3((tot + 255) / 256), dim3(256), 0, s, n_rows,
+                       width, (const float*)src, lds, (float*)cache, row_stride, req_stride,
+                       row_req, row_pos);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_kv_scatter: dtype");
+  SMER_CHECK_LAUNCH("smer_kv_scatter");
+  return SMER_OK;
+}

@@ -1,0 +1,74 @@
+"""Build libsmer_hip.so (gfx950) in-tree with hipcc.
+
+    python -m smer_music_generation_amd.csrc.build      # or build() below
+
+Each .hip/.cpp is compiled to an object under csrc/_build/ (skipped when
+up to date) and linked into smer_music_generation_amd/libsmer_hip.so.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+OUT = os.path.join(PKG, "libsmer_hip.so")
+OBJ = os.path.join(HERE, "_build")
+SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm_embed.hip", "train_ops.hip"]
+HEADERS = ["common.h", os.path.join("..", "..", "include", "smer_hip.h")]
+ARCH = os.environ.get("SMER_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build libsmer_hip.so)")
+
+
+def _flags():
+    return ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
+            "-Wno-unused-result", "-I" + os.path.join(ROOT, "include")]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+    deps = [os.path.join(HERE, src)] + [os.path.join(HERE, h) for h in HEADERS]
+    if not _newer(obj, deps):
+        return obj
+    cmd = [_hipcc()] + _flags() + ["-c", os.path.join(HERE, src), "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("hipcc failed for %s:\n%s\n%s" % (src, " ".join(cmd), r.stderr))
+    return obj
+
+
+def build(verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    jobs = min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if _newer(OUT, objs):
+        cmd = [_hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", OUT]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s" % (" ".join(cmd), r.stderr))
+    if verbose:
+        print("built", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

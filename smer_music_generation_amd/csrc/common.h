@@ -1,0 +1,77 @@
+// Shared device helpers for the SMER gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/smer_hip.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define SMER_WAVE 64
+
+// status reporting (defined in abi.cpp)
+extern "C" int smer_set_error(int code, const char* msg);
+#define SMER_CHECK_LAUNCH(what)                                          \
+  do {                                                                   \
+    hipError_t _e = hipGetLastError();                                   \
+    if (_e != hipSuccess) return smer_set_error(SMER_ERR_HIP, hipGetErrorString(_e)); \
+  } while (0)
+#define SMER_REQUIRE(cond, msg) \
+  do { if (!(cond)) return smer_set_error(SMER_ERR_INVALID, msg); } while (0)
+
+template <typename T> __device__ __forceinline__ float to_f32(T x);
+template <> __device__ __forceinline__ float to_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ float to_f32<bf16>(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based dropout hash: keep iff hash(seed, row, col) >= threshold,
+// threshold = p * 2^32.  Same function in every forward/backward site.
+__device__ __forceinline__ uint32_t smer_hash3(uint32_t seed, uint32_t a, uint32_t b) {
+  uint32_t h = seed ^ 0x9E3779B9u;
+  h ^= a * 0xCC9E2D51u; h = (h << 15) | (h >> 17); h *= 0x1B873593u;
+  h ^= b * 0x85EBCA6Bu; h = (h << 13) | (h >> 19); h = h * 5u + 0xE6546B64u;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ bool smer_keep(uint32_t seed, uint32_t thr, uint32_t a, uint32_t b) {
+  return smer_hash3(seed, a, b) >= thr;
+}
+static inline uint32_t smer_drop_threshold(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 4294967296.0;
+  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+__device__ __forceinline__ bf16x8 lds_read_b128(const char* base, uint32_t byte_off) {
+  return *reinterpret_cast<const bf16x8*>(base + byte_off);
+}
+// gfx950 ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q,
+// columns 4p..4p+3 of a 4x16 block; lane i receives column i (rows 0..3).
+__device__ __forceinline__ bf16x4 lds_read_tr16(const char* base, uint32_t byte_off) {
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + byte_off));
+  return __builtin_bit_cast(bf16x4, r);
+}
+__device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}

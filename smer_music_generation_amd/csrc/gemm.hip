@@ -1,0 +1,307 @@
+// GEMM for every projection of the SMER Transformer (QKV in-proj, out-proj,
+// FFN, vocab head) and their dgrad / wgrad.
+//
+// bf16 path: 128x128x64 block tile, 4 waves (2x2, 64x64 each),
+// mfma_f32_16x16x32_bf16, register-staged double-buffered LDS (issue the
+// next tile's global loads before the MFMAs, write LDS after them).
+// Either operand may be K-contiguous ("row" image, XOR-swizzled 16-B chunks,
+// ds_read_b128 fragments) or M/N-contiguous ("column" image, 8-B units
+// XOR-swizzled, ds_read_b64_tr_b16 transposing fragments) — so forward (NT),
+// dgrad (NN) and wgrad (TN) all run without an explicit transpose pass.
+// f32 path (parity mode): LDS-tiled VALU FMA, same epilogue.
+#include "common.h"
+
+struct GemmEpi {
+  const float* bias;
+  float alpha;
+  int relu;
+  const void* residual;
+  long ldr;
+  const void* gate;
+  long ldg;
+  float gate_scale;
+  uint32_t drop_thr;
+  uint32_t seed;
+  float drop_scale;
+  void* C;
+  long ldc;
+  float* Cf;
+  long ldcf;
+  int accumulate;
+};
+
+template <typename T>
+__device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int row, int col,
+                                          float acc) {
+  if (row >= M || col >= N) return;
+  float v = acc * e.alpha;
+  if (e.bias) v += e.bias[col];
+  if (e.relu) v = fmaxf(v, 0.f);
+  if (e.drop_thr) v = smer_keep(e.seed, e.drop_thr, (uint32_t)row, (uint32_t)col) ? v * e.drop_scale : 0.f;
+  if (e.residual) v += to_f32(((const T*)e.residual)[(long)row * e.ldr + col]);
+  if (e.gate) {
+    float gv = to_f32(((const T*)e.gate)[(long)row * e.ldg + col]);
+    v = gv > 0.f ? v * e.gate_scale : 0.f;
+  }
+  if (e.C) ((T*)e.C)[(long)row * e.ldc + col] = from_f32<T>(v);
+  if (e.Cf) {
+    float* p = e.Cf + (long)row * e.ldcf + col;
+    *p = e.accumulate ? *p + v : v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 MFMA kernel
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int GBM = 128, GBN = 128, GBK = 64;
+constexpr int TILE_BYTES = GBM * GBK * 2;  // 16 KiB per operand per buffer
+
+__device__ __forceinline__ uint32_t col_swz(int k) {  // 3-bit row signature
+  return (uint32_t)((k & 3) | (((k >> 3) & 1) << 2));
+}
+
+// Stage one operand tile (rows r0.., k0..) into registers.
+// KC: operand stored [rows][K]; else stored [K][rows].
+template <bool KC>
+__device__ __forceinline__ void stage_load(uint4 (&r)[4], const bf16* P, long ld, int rows,
+                                           int K, int r0, int k0, int tid) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int i = tid + 256 * c;
+    int gr, gk;
+    if (KC) { gr = r0 + (i >> 3); gk = k0 + (i & 7) * 8; }
+    else    { gk = k0 + (i >> 4); gr = r0 + (i & 15) * 8; }
+    bool ok = gr < rows && gk < K;
+    const bf16* src = KC ? P + (long)gr * ld + gk : P + (long)gk * ld + gr;
+    r[c] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void stage_store(const uint4 (&r)[4], char* buf, int tid) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int i = tid + 256 * c;
+    uint32_t off;
+    if (KC) {
+      int row = i >> 3, ch = i & 7;
+      off = row * 128 + ((ch ^ (row & 7)) << 4);
+    } else {
+      int k = i >> 4, ch = i & 15;
+      off = k * 256 + ((ch ^ (2 * col_swz(k))) << 4);
+    }
+    *reinterpret_cast<uint4*>(buf + off) = r[c];
+  }
+}
+
+// Fragment (16 rows starting at rbase, k-step s) for lane l.
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int lane) {
+  int g = lane >> 4, c16 = lane & 15;
+  if (KC) {
+    int row = rbase + c16;
+    int ch = s * 4 + g;
+    return lds_read_b128(buf, row * 128 + ((ch ^ (row & 7)) << 4));
+  } else {
+    int q = c16 >> 2, p = c16 & 3;
+    int u = (rbase >> 2) + p;
+    int k0 = s * 32 + 8 * g + q;
+    int k1 = k0 + 4;
+    bf16x4 lo = lds_read_tr16(buf, k0 * 256 + ((u ^ (4 * col_swz(k0))) << 3));
+    bf16x4 hi = lds_read_tr16(buf, k1 * 256 + ((u ^ (4 * col_swz(k1))) << 3));
+    return cat4(lo, hi);
+  }
+}
+}  // namespace
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
+                                                           const bf16* __restrict__ A, long lda,
+                                                           const bf16* __restrict__ B, long ldb,
+                                                           GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbm = (M + GBM - 1) / GBM, nbn = (N + GBN - 1) / GBN;
+  const int nwg = nbm * nbn;
+  // bijective XCD remap (blocks b and b+8 share an XCD): give each XCD a
+  // contiguous run of tiles, then walk tiles in GM-row groups for L2 reuse.
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GM = 8;
+  const int grp = wgid / (GM * nbn);
+  const int first_m = grp * GM;
+  const int gsz = min(nbm - first_m, GM);
+  const int within = wgid % (GM * nbn);
+  const int tm = first_m + within % gsz, tn = within / gsz;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+
+  // buffer b: A at smem + b*2*TILE_BYTES, B right after it
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  const int nk = (K + GBK - 1) / GBK;
+  stage_load<AK>(ra, A, lda, M, K, m0, 0, tid);
+  stage_load<BKC>(rb, B, ldb, N, K, n0, 0, tid);
+  stage_store<AK>(ra, smem, tid);
+  stage_store<BKC>(rb, smem + TILE_BYTES, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      stage_load<AK>(ra, A, lda, M, K, m0, (kt + 1) * GBK, tid);
+      stage_load<BKC>(rb, B, ldb, N, K, n0, (kt + 1) * GBK, tid);
+    }
+    const char* a_s = smem + cur * 2 * TILE_BYTES;
+    const char* b_s = a_s + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(a_s, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (more) {
+      stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
+      stage_store<BKC>(rb, smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES, tid);
+    }
+    __syncthreads();
+  }
+
+  const int g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        epi_apply<bf16>(e, M, N, m0 + wm * 64 + i * 16 + 4 * g + r, n0 + wn * 64 + j * 16 + c16,
+                        acc[i][j][r]);
+}
+
+// ---------------------------------------------------------------------------
+// f32 VALU kernel (parity mode)
+// ---------------------------------------------------------------------------
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K,
+                                                       const float* __restrict__ A, long lda,
+                                                       const float* __restrict__ B, long ldb,
+                                                       GemmEpi e) {
+  __shared__ float As[16][68];
+  __shared__ float Bs[16][68];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      int i = tid + 256 * c;
+      int m, kk;
+      if (AK) { m = i >> 4; kk = i & 15; } else { kk = i >> 6; m = i & 63; }
+      int gm = m0 + m, gk = k0 + kk;
+      float a = 0.f;
+      if (gm < M && gk < K) a = AK ? A[(long)gm * lda + gk] : A[(long)gk * lda + gm];
+      As[kk][m] = a;
+      int n;
+      if (BKC) { n = i >> 4; kk = i & 15; } else { kk = i >> 6; n = i & 63; }
+      int gn = n0 + n;
+      gk = k0 + kk;
+      float b = 0.f;
+      if (gn < N && gk < K) b = BKC ? B[(long)gn * ldb + gk] : B[(long)gk * ldb + gn];
+      Bs[kk][n] = b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_apply<float>(e, M, N, m0 + ty * 4 + i, n0 + tx * 4 + j, acc[i][j]);
+}
+
+// ---------------------------------------------------------------------------
+template <bool AK, bool BKC>
+static void launch_bf16(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                        const GemmEpi& e, hipStream_t s) {
+  int nwg = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC>), dim3(nwg), dim3(256), 4 * TILE_BYTES, s, M, N,
+                     K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+}
+template <bool AK, bool BKC>
+static void launch_f32(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                       const GemmEpi& e, hipStream_t s) {
+  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC>), grid, dim3(256), 0, s, M, N, K,
+                     (const float*)A, lda, (const float*)B, ldb, e);
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
+                         const void* A, long lda, const void* B, long ldb, const float* bias,
+                         float alpha, int relu, const void* residual, long ldr, const void* gate,
+                         long ldg, float gate_scale, float drop_p, uint32_t drop_seed, void* C,
+                         long ldc, float* Cf, long ldcf, int accumulate, smer_stream_t stream) {
+  SMER_REQUIRE(M >= 0 && N >= 0 && K >= 0, "smer_gemm: negative size");
+  SMER_REQUIRE(A && B, "smer_gemm: null operand");
+  SMER_REQUIRE(C || Cf, "smer_gemm: no output");
+  SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_gemm: drop_p out of range");
+  if (M == 0 || N == 0) return SMER_OK;
+  GemmEpi e;
+  e.bias = bias; e.alpha = alpha; e.relu = relu; e.residual = residual; e.ldr = ldr;
+  e.gate = gate; e.ldg = ldg; e.gate_scale = gate_scale;
+  e.drop_thr = smer_drop_threshold(drop_p); e.seed = drop_seed;
+  e.drop_scale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf; e.accumulate = accumulate;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == SMER_BF16) {
+    SMER_REQUIRE(K % 8 == 0, "smer_gemm(bf16): K must be a multiple of 8");
+    SMER_REQUIRE(lda % 8 == 0 && ldb % 8 == 0, "smer_gemm(bf16): lda/ldb must be multiples of 8");
+    SMER_REQUIRE(aligned16(A) && aligned16(B), "smer_gemm(bf16): operands must be 16-B aligned");
+    SMER_REQUIRE(a_kcontig || lda >= (long)((M + 7) / 8) * 8,
+                 "smer_gemm(bf16): column-image A needs lda >= round_up(M, 8)");
+    SMER_REQUIRE(b_kcontig || ldb >= (long)((N + 7) / 8) * 8,
+                 "smer_gemm(bf16): column-image B needs ldb >= round_up(N, 8)");
+    if (K == 0) return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm: K == 0");
+    if (a_kcontig && b_kcontig) launch_bf16<true, true>(M, N, K, A, lda, B, ldb, e, s);
+    else if (a_kcontig) launch_bf16<true, false>(M, N, K, A, lda, B, ldb, e, s);
+    else if (b_kcontig) launch_bf16<false, true>(M, N, K, A, lda, B, ldb, e, s);
+    else launch_bf16<false, false>(M, N, K, A, lda, B, ldb, e, s);
+  } else if (dtype == SMER_F32) {
+    if (a_kcontig && b_kcontig) launch_f32<true, true>(M, N, K, A, lda, B, ldb, e, s);
+    else if (a_kcontig) launch_f32<true, false>(M, N, K, A, lda, B, ldb, e, s);
+    else if (b_kcontig) launch_f32<false, true>(M, N, K, A, lda, B, ldb, e, s);
+    else launch_f32<false, false>(M, N, K, A, lda, B, ldb, e, s);
+  } else {
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm: dtype");
+  }
+  SMER_CHECK_LAUNCH("smer_gemm");
+  return SMER_OK;
+}

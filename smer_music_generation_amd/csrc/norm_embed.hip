@@ -1,0 +1,395 @@
+// LayerNorm (post-LN residual blocks, eps 1e-5; transformer.py:392,395,462,
+// 466,469 and the final norms 274-275, 329-330) and the embedding + PE
+// front end (model.py:91-92, 124-125).  All HBM-bound: one wave per row,
+// 16-B vector loads, fp32 math, deterministic two-stage column reductions
+// for dgamma / dbeta / dtable.
+#include "common.h"
+
+namespace {
+constexpr int LN_MAXC = 4;  // 16-B chunks per lane: N <= 64*8*4 = 2048
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float (&v)[8]) {
+    bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)r[i];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float (&v)[8]) {
+    bf16x8 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = (bf16)v[i];
+    *reinterpret_cast<bf16x8*>(p) = r;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+}  // namespace
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __restrict__ x, long ldx,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     T* __restrict__ y, long ldy,
+                                                     float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nch = N >> 3;
+  float v[LN_MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c) {
+    int ch = lane + 64 * c;
+    if (ch < nch) {
+      Vec8<T>::load(x + (long)row * ldx + ch * 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  const float mu = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { float d = v[c][i] - mu; q += d * d; }
+  const float rs = rsqrtf(wave_sum(q) / N + eps);
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c) {
+    int ch = lane + 64 * c;
+    if (ch < nch) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * rs * gamma[ch * 8 + i] + beta[ch * 8 + i];
+      Vec8<T>::store(y + (long)row * ldy + ch * 8, o);
+    }
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+constexpr int LN_BWD_ROWS = 64;  // rows per workgroup (16 per wave)
+
+template <typename T, bool DYF>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* __restrict__ dyv,
+                                                     long lddy, const T* __restrict__ x, long ldx,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma,
+                                                     T* __restrict__ dx, long lddx,
+                                                     T* __restrict__ dxd, long ldxd,
+                                                     uint32_t thr, uint32_t seed, float dscale,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][2][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nch = N >> 3;
+  float pg[LN_MAXC][8], pb[LN_MAXC][8];
+#pragma unroll
+  for (int c = 0; c < LN_MAXC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { pg[c][i] = 0.f; pb[c][i] = 0.f; }
+  const int r0 = blockIdx.x * LN_BWD_ROWS;
+  for (int rr = wave; rr < LN_BWD_ROWS; rr += 4) {
+    const int row = r0 + rr;
+    if (row >= M) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[LN_MAXC][8], gd[LN_MAXC][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        float xv[8], dv[8];
+        Vec8<T>::load(x + (long)row * ldx + ch * 8, xv);
+        if (DYF) Vec8<float>::load((const float*)dyv + (long)row * lddy + ch * 8, dv);
+        else Vec8<T>::load((const T*)dyv + (long)row * lddy + ch * 8, dv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float h = (xv[i] - mu) * rs;
+          float gg = dv[i] * gamma[ch * 8 + i];
+          xh[c][i] = h;
+          gd[c][i] = gg;
+          s1 += gg;
+          s2 += gg * h;
+          pg[c][i] += dv[i] * h;
+          pb[c][i] += dv[i];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / N;
+    s2 = wave_sum(s2) / N;
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rs * (gd[c][i] - s1 - xh[c][i] * s2);
+        Vec8<T>::store(dx + (long)row * lddx + ch * 8, o);
+        if (dxd) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            o[i] = (thr == 0u || smer_keep(seed, thr, (uint32_t)row, (uint32_t)(ch * 8 + i))) ? o[i] * dscale : 0.f;
+          Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
+        }
+      }
+    }
+  }
+  if (!part) return;
+  // combine the 4 waves' column partials in fixed order, in <=512-col slabs
+  for (int base = 0; base < N; base += 512) {
+#pragma unroll
+    for (int c = 0; c < LN_MAXC; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch && ch * 8 >= base && ch * 8 < base + 512)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          red[wave][0][ch * 8 + i - base] = pg[c][i];
+          red[wave][1][ch * 8 + i - base] = pb[c][i];
+        }
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < 512 && base + col < N; col += 256) {
+      float a = (red[0][0][col] + red[1][0][col]) + (red[2][0][col] + red[3][0][col]);
+      float b = (red[0][1][col] + red[1][1][col]) + (red[2][1][col] + red[3][1][col]);
+      part[(long)blockIdx.x * 2 * N + base + col] = a;
+      part[(long)blockIdx.x * 2 * N + N + base + col] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// out[col] (+)= sum_b part[b*stride + off + col]
+__global__ void col_reduce_kernel(int nblk, int N, const float* __restrict__ part, long stride,
+                                  long off, float* __restrict__ out, int accumulate, float scale) {
+  int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  float a = 0.f;
+  for (int b = 0; b < nblk; ++b) a += part[(long)b * stride + off + col];
+  a *= scale;
+  out[col] = accumulate ? out[col] + a : a;
+}
+
+// ---------------------------------------------------------------------------
+// embedding + sinusoidal PE
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void embed_fwd_kernel(int n_tok, int d, const int64_t* __restrict__ ids,
+                                 const int32_t* __restrict__ positions, int L,
+                                 const float* __restrict__ table, const float* __restrict__ pe,
+                                 float scale, uint32_t thr, uint32_t seed, float dscale,
+                                 T* __restrict__ out, long ldo) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = d >> 2;
+  if (idx >= (long)n_tok * per) return;
+  int t = idx / per, c = (idx % per) * 4;
+  long id = ids[t];
+  int pos = positions ? positions[t] : t % L;
+  float4 e = *reinterpret_cast<const float4*>(table + id * d + c);
+  float4 p = *reinterpret_cast<const float4*>(pe + (long)pos * d + c);
+  float v[4] = {e.x * scale + p.x, e.y * scale + p.y, e.z * scale + p.z, e.w * scale + p.w};
+  T* o = out + (long)t * ldo + c;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float w = v[i];
+    if (thr) w = smer_keep(seed, thr, (uint32_t)t, (uint32_t)(c + i)) ? w * dscale : 0.f;
+    o[i] = from_f32<T>(w);
+  }
+}
+
+constexpr int EMB_CHUNK = 512;  // tokens per workgroup in the per-vocab gather
+
+// part[chunk][v][:] = sum over tokens t of this chunk with id v of dx[t] * keep
+template <typename T>
+__global__ __launch_bounds__(256) void embed_bwd_gather(
+    int V, int d, const int64_t* __restrict__ ids0, const T* __restrict__ dx0, long ld0, int n0,
+    uint32_t thr0, uint32_t seed0, float ds0, const int64_t* __restrict__ ids1,
+    const T* __restrict__ dx1, long ld1, int n1, uint32_t thr1, uint32_t seed1, float ds1,
+    float* __restrict__ part) {
+  __shared__ float red[4][1024];
+  const int v = blockIdx.x, chunk = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ncol = d / 64;  // columns per lane (d % 64 == 0, d <= 1024)
+  float acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const int n = n0 + n1;
+  const int t_begin = chunk * EMB_CHUNK + wave * (EMB_CHUNK / 4);
+  for (int g0 = t_begin; g0 < t_begin + EMB_CHUNK / 4 && g0 < n; g0 += 64) {
+    int t = g0 + lane;
+    bool hit = false;
+    if (t < n) hit = (t < n0 ? ids0[t] : ids1[t - n0]) == v;
+    unsigned long long mask = __ballot(hit);
+    while (mask) {
+      int b = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      int tt = g0 + b;
+      const bool s0 = tt < n0;
+      const int tl = s0 ? tt : tt - n0;
+      const uint32_t thr = s0 ? thr0 : thr1;
+      const uint32_t sd = s0 ? seed0 : seed1;
+      const float dsc = s0 ? ds0 : ds1;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (i < ncol) {
+          int col = lane + 64 * i;
+          float g = s0 ? to_f32(dx0[(long)tl * ld0 + col]) : to_f32(dx1[(long)tl * ld1 + col]);
+          if (thr) g = smer_keep(sd, thr, (uint32_t)tl, (uint32_t)col) ? g * dsc : 0.f;
+          acc[i] += g;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < ncol) red[wave][lane + 64 * i] = acc[i];
+  __syncthreads();
+  float* dst = part + ((long)chunk * V + v) * d;
+  for (int col = threadIdx.x; col < d; col += 256)
+    dst[col] = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
+}
+
+__global__ void embed_bwd_reduce(int V, int d, int nchunk, const float* __restrict__ part,
+                                 float scale, float* __restrict__ dtable) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)V * d) return;
+  float a = 0.f;
+  for (int c = 0; c < nchunk; ++c) a += part[(long)c * V * d + idx];
+  dtable[idx] += a * scale;
+}
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long ldx,
+                                  const float* gamma, const float* beta, float eps, void* y,
+                                  long ldy, float* mean, float* rstd, smer_stream_t stream) {
+  SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_fwd: N % 8 == 0 and N <= 2048");
+  SMER_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0, "smer_layernorm_fwd: strides % 8");
+  if (M == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4);
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma,
+                       beta, eps, (bf16*)y, ldy, mean, rstd);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, grid, dim3(256), 0, s, M, N, (const float*)x, ldx,
+                       gamma, beta, eps, (float*)y, ldy, mean, rstd);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_fwd: dtype");
+  SMER_CHECK_LAUNCH("smer_layernorm_fwd");
+  return SMER_OK;
+}
+
+extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
+  size_t nblk = (size_t)(M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  return nblk * 2 * N * sizeof(float);
+}
+
+extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
+                                  const void* x, long ldx, const float* mean, const float* rstd,
+                                  const float* gamma, void* dx, long lddx, void* dx_drop,
+                                  long ldxd, float drop_p, uint32_t seed, float* dgamma,
+                                  float* dbeta, int accumulate, void* workspace, size_t ws_bytes,
+                                  smer_stream_t stream) {
+  SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_bwd: N % 8 == 0 and N <= 2048");
+  SMER_REQUIRE(dx && dy && x && mean && rstd && gamma, "smer_layernorm_bwd: null pointer");
+  bool params = dgamma || dbeta;
+  SMER_REQUIRE(!params || (workspace && ws_bytes >= smer_layernorm_bwd_workspace(M, N)),
+               "smer_layernorm_bwd: workspace too small");
+  if (M == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int nblk = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  uint32_t thr = smer_drop_threshold(drop_p);
+  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  float* part = params ? (float*)workspace : nullptr;
+#define LNB(T, F)                                                                              \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, F>), dim3(nblk), dim3(256), 0, s, M, N, dy, lddy,       \
+                     (const T*)x, ldx, mean, rstd, gamma, (T*)dx, lddx, (T*)dx_drop, ldxd, thr, \
+                     seed, ds, part)
+  if (dtype == SMER_BF16) { if (dy_f32) LNB(bf16, true); else LNB(bf16, false); }
+  else if (dtype == SMER_F32) { LNB(float, false); }
+  else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
+#undef LNB
+  if (dgamma)
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N, part,
+                       (long)2 * N, 0L, dgamma, accumulate, 1.f);
+  if (dbeta)
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N, part,
+                       (long)2 * N, (long)N, dbeta, accumulate, 1.f);
+  SMER_CHECK_LAUNCH("smer_layernorm_bwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_embed_fwd(int dtype, int n_tok, int d, const int64_t* ids,
+                              const int32_t* positions, int L, const float* table,
+                              const float* pe, float scale, float drop_p, uint32_t seed,
+                              void* out, long ldo, smer_stream_t stream) {
+  SMER_REQUIRE(d % 4 == 0, "smer_embed_fwd: d % 4 == 0");
+  SMER_REQUIRE(positions || L > 0, "smer_embed_fwd: L");
+  if (n_tok == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  long tot = (long)n_tok * (d / 4);
+  uint32_t thr = smer_drop_threshold(drop_p);
+  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3((tot + 255) / 256), dim3(256), 0, s, n_tok, d,
+                       ids, positions, L, table, pe, scale, thr, seed, ds, (bf16*)out, ldo);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(embed_fwd_kernel<float>, dim3((tot + 255) / 256), dim3(256), 0, s, n_tok, d,
+                       ids, positions, L, table, pe, scale, thr, seed, ds, (float*)out, ldo);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_embed_fwd: dtype");
+  SMER_CHECK_LAUNCH("smer_embed_fwd");
+  return SMER_OK;
+}
+
+extern "C" size_t smer_embed_bwd_workspace(int V, int d, int n_tok_total) {
+  size_t nchunk = (size_t)(n_tok_total + EMB_CHUNK - 1) / EMB_CHUNK;
+  if (nchunk == 0) nchunk = 1;
+  return nchunk * V * d * sizeof(float);
+}
+
+extern "C" int smer_embed_bwd(int dtype, int V, int d, float scale, const int64_t* ids0,
+                              const void* dx0, long ld0, int n0, float p0, uint32_t seed0,
+                              const int64_t* ids1, const void* dx1, long ld1, int n1, float p1,
+                              uint32_t seed1, float* dtable, void* workspace, size_t ws_bytes,
+                              smer_stream_t stream) {
+  SMER_REQUIRE(d % 64 == 0 && d <= 1024, "smer_embed_bwd: d % 64 == 0 and d <= 1024");
+  SMER_REQUIRE(workspace && ws_bytes >= smer_embed_bwd_workspace(V, d, n0 + n1),
+               "smer_embed_bwd: workspace too small");
+  int n = n0 + n1;
+  if (n == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int nchunk = (n + EMB_CHUNK - 1) / EMB_CHUNK;
+  uint32_t t0 = smer_drop_threshold(p0), t1 = smer_drop_threshold(p1);
+  float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
+  dim3 grid(V, nchunk);
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(embed_bwd_gather<bf16>, grid, dim3(256), 0, s, V, d, ids0, (const bf16*)dx0,
+                       ld0, n0, t0, seed0, ds0, ids1, (const bf16*)dx1, ld1, n1, t1, seed1, ds1,
+                       (float*)workspace);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(embed_bwd_gather<float>, grid, dim3(256), 0, s, V, d, ids0,
+                       (const float*)dx0, ld0, n0, t0, seed0, ds0, ids1, (const float*)dx1, ld1,
+                       n1, t1, seed1, ds1, (float*)workspace);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_embed_bwd: dtype");
+  long tot = (long)V * d;
+  hipLaunchKernelGGL(embed_bwd_reduce, dim3((tot + 255) / 256), dim3(256), 0, s, V, d, nchunk,
+                     (const float*)workspace, scale, dtable);
+  SMER_CHECK_LAUNCH("smer_embed_bwd");
+  return SMER_OK;
+}

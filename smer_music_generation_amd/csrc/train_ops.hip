@@ -1,0 +1,216 @@
+// Training-step tail: the fused multi-criterion weighted cross entropy
+// (train.py:555-642, 726-780), torch.optim.Adam (train.py:264, 786), bias
+// gradient column sums and dtype casts.  All HBM-bound elementwise / row
+// kernels; reductions are fixed-order (bitwise reproducible).
+#include "common.h"
+
+// denom = sum_i ce_all[y_i]   (single workgroup, fixed order)
+__global__ __launch_bounds__(256) void wce_denom_kernel(int n, const int64_t* __restrict__ y,
+                                                        const float* __restrict__ ce_all,
+                                                        float* __restrict__ denom) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) a += ce_all[y[i]];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *denom = red[0];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void wce_kernel(int R, int V, const float* __restrict__ logits,
+                                                  long ldl, const int64_t* __restrict__ y,
+                                                  const float* __restrict__ w,
+                                                  const float* __restrict__ denom,
+                                                  float* __restrict__ row_loss,
+                                                  T* __restrict__ dlog, long ldd,
+                                                  float grad_scale) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* x = logits + (long)r * ldl;
+  const long yt = y[r];
+  float mx = -INFINITY;
+  for (int v = lane; v < V; v += 64) mx = fmaxf(mx, x[v]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int v = lane; v < V; v += 64) se += expf(x[v] - mx);
+  se = wave_sum(se);
+  const float lse = mx + logf(se);
+  const float wy = yt == 0 ? 0.f : w[yt];
+  if (lane == 0) row_loss[r] = wy * (lse - x[yt]);
+  if (dlog) {
+    const float coef = grad_scale * wy / *denom;
+    const float inv = 1.f / se;
+    for (int v = lane; v < V; v += 64) {
+      float g = coef * (expf(x[v] - mx) * inv - (v == yt ? 1.f : 0.f));
+      dlog[(long)r * ldd + v] = from_f32<T>(g);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sum_div_kernel(int n, const float* __restrict__ x,
+                                                      const float* __restrict__ denom,
+                                                      float* __restrict__ out) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) a += x[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = denom ? red[0] / *denom : red[0];
+}
+
+// torch.optim.Adam (_single_tensor_adam): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                            float* __restrict__ m, float* __restrict__ v, bf16* __restrict__ pb,
+                            float lr, float b1, float b2, float eps, float bc1, float bc2s) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  const float step = lr / bc1;
+  for (; i < n; i += stride) {
+    float gi = g[i];
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    float den = sqrtf(vi) / bc2s + eps;
+    float pi = p[i] - step * (mi / den);
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (pb) pb[i] = (bf16)pi;
+  }
+}
+
+template <typename S, typename D>
+__global__ void cast_kernel(long n, const S* __restrict__ s, D* __restrict__ d) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) d[i] = from_f32<D>(to_f32(s[i]));
+}
+
+constexpr int CS_ROWS = 128;
+template <typename T>
+__global__ void colsum_part_kernel(int M, int N, const T* __restrict__ x, long ldx,
+                                   float* __restrict__ part) {
+  int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  int r0 = blockIdx.y * CS_ROWS;
+  int r1 = min(M, r0 + CS_ROWS);
+  float a = 0.f;
+  for (int r = r0; r < r1; ++r) a += to_f32(x[(long)r * ldx + col]);
+  part[(long)blockIdx.y * N + col] = a;
+}
+__global__ void colsum_final_kernel(int nblk, int N, const float* __restrict__ part,
+                                    float* __restrict__ out, int accumulate) {
+  int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  float a = 0.f;
+  for (int b = 0; b < nblk; ++b) a += part[(long)b * N + col];
+  out[col] = accumulate ? out[col] + a : a;
+}
+
+// ---------------------------------------------------------------------------
+extern "C" int smer_wce_denom(int n, const int64_t* y, const float* ce_all, float* denom,
+                              smer_stream_t stream) {
+  SMER_REQUIRE(y && ce_all && denom, "smer_wce_denom: null pointer");
+  hipLaunchKernelGGL(wce_denom_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n, y, ce_all,
+                     denom);
+  SMER_CHECK_LAUNCH("smer_wce_denom");
+  return SMER_OK;
+}
+
+extern "C" int smer_wce_fwd_bwd(int dtype, int R, int V, const float* logits, long ldl,
+                                const int64_t* y, const float* w, const float* denom,
+                                float* row_loss, float* loss_out, void* dlogits, long ldd,
+                                float grad_scale, smer_stream_t stream) {
+  SMER_REQUIRE(logits && y && w && denom && row_loss, "smer_wce_fwd_bwd: null pointer");
+  if (R == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((R + 3) / 4);
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(wce_kernel<bf16>, grid, dim3(256), 0, s, R, V, logits, ldl, y, w, denom,
+                       row_loss, (bf16*)dlogits, ldd, grad_scale);
+  else if (dtype == SMER_F32)
+    hipLaunchKernelGGL(wce_kernel<float>, grid, dim3(256), 0, s, R, V, logits, ldl, y, w, denom,
+                       row_loss, (float*)dlogits, ldd, grad_scale);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_wce_fwd_bwd: dtype");
+  if (loss_out)
+    hipLaunchKernelGGL(sum_div_kernel, dim3(1), dim3(256), 0, s, R, row_loss, denom, loss_out);
+  SMER_CHECK_LAUNCH("smer_wce_fwd_bwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_adam(long n, float* p, const float* g, float* m, float* v, void* p_bf16,
+                         float lr, float b1, float b2, float eps, float bc1, float bc2_sqrt,
+                         smer_stream_t stream) {
+  SMER_REQUIRE(p && g && m && v, "smer_adam: null pointer");
+  if (n == 0) return SMER_OK;
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v,
+                     (bf16*)p_bf16, lr, b1, b2, eps, bc1, bc2_sqrt);
+  SMER_CHECK_LAUNCH("smer_adam");
+  return SMER_OK;
+}
+
+extern "C" int smer_cast(int src_dtype, int dst_dtype, long n, const void* src, void* dst,
+                         smer_stream_t stream) {
+  if (n == 0) return SMER_OK;
+  long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  if (src_dtype == SMER_F32 && dst_dtype == SMER_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(blocks), dim3(256), 0, s, n,
+                       (const float*)src, (bf16*)dst);
+  else if (src_dtype == SMER_BF16 && dst_dtype == SMER_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(blocks), dim3(256), 0, s, n,
+                       (const bf16*)src, (float*)dst);
+  else if (src_dtype == SMER_F32 && dst_dtype == SMER_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(blocks), dim3(256), 0, s, n,
+                       (const float*)src, (float*)dst);
+  else if (src_dtype == SMER_BF16 && dst_dtype == SMER_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(blocks), dim3(256), 0, s, n,
+                       (const bf16*)src, (bf16*)dst);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_cast: dtype");
+  SMER_CHECK_LAUNCH("smer_cast");
+  return SMER_OK;
+}
+
+extern "C" size_t smer_colsum_workspace(int M, int N) {
+  return (size_t)((M + CS_ROWS - 1) / CS_ROWS) * N * sizeof(float);
+}
+
+extern "C" int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out,
+                           int accumulate, void* workspace, size_t ws_bytes,
+                           smer_stream_t stream) {
+  SMER_REQUIRE(x && out, "smer_colsum: null pointer");
+  SMER_REQUIRE(workspace && ws_bytes >= smer_colsum_workspace(M, N), "smer_colsum: workspace");
+  if (N == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int nblk = (M + CS_ROWS - 1) / CS_ROWS;
+  dim3 grid((N + 255) / 256, nblk > 0 ? nblk : 1);
+  if (M > 0) {
+    if (dtype == SMER_BF16)
+      hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)x,
+                         ldx, (float*)workspace);
+    else if (dtype == SMER_F32)
+      hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, s, M, N,
+                         (const float*)x, ldx, (float*)workspace);
+    else
+      return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_colsum: dtype");
+  }
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N,
+                     (const float*)workspace, out, accumulate);
+  SMER_CHECK_LAUNCH("smer_colsum");
+  return SMER_OK;
+}

@@ -1,0 +1,209 @@
+"""Tensor-level wrappers over the C-ABI (one function per entry point).
+
+Every wrapper takes torch tensors already on the GPU, passes raw pointers,
+row strides and torch's current HIP stream to libsmer_hip.so and raises
+`SmerError` on a non-zero status.  There is no CPU or ATen fallback: a CPU
+tensor is rejected, a missing library raises at first use.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, load
+
+F32, BF16 = 0, 1
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return F32
+    if t == torch.bfloat16:
+        return BF16
+    raise TypeError("unsupported dtype %s" % t)
+
+
+def _p(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("smer op: tensor must be on the GPU (got %s)" % t.device)
+    return t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld(t):
+    """Row stride (elements) of a 2-D view with unit column stride."""
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise RuntimeError("smer op: expected a 2-D row-major view, got strides %s" % (t.stride(),))
+    return t.stride(0)
+
+
+# ---------------------------------------------------------------------------
+def gemm(A, B, *, M, N, K, a_kcontig=True, b_kcontig=True, out=None, out_f32=None,
+         accumulate=False, bias=None, alpha=1.0, relu=False, residual=None, gate=None,
+         gate_scale=1.0, drop_p=0.0, seed=0, dtype=None):
+    """out (+)= epilogue(alpha * op(A) op(B)^T); see include/smer_hip.h."""
+    dt = dtype_code(dtype if dtype is not None else A.dtype)
+    call("smer_gemm", dt, int(a_kcontig), int(b_kcontig), M, N, K, _p(A), _ld(A), _p(B), _ld(B),
+         _p(bias), float(alpha), int(relu), _p(residual),
+         _ld(residual) if residual is not None else 0, _p(gate),
+         _ld(gate) if gate is not None else 0, float(gate_scale), float(drop_p),
+         int(seed) & 0xFFFFFFFF, _p(out), _ld(out) if out is not None else 0, _p(out_f32),
+         _ld(out_f32) if out_f32 is not None else 0, int(accumulate), _stream())
+
+
+def linear(x, w, bias=None, *, out=None, out_f32=None, accumulate=False, relu=False,
+           residual=None, drop_p=0.0, seed=0):
+    """y = x @ w^T (+bias ...): x [M,K], w [N,K]."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None and out_f32 is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    gemm(x, w, M=M, N=N, K=K, out=out, out_f32=out_f32, accumulate=accumulate, bias=bias,
+         relu=relu, residual=residual, drop_p=drop_p, seed=seed, dtype=x.dtype)
+    return out if out is not None else out_f32
+
+
+def linear_dgrad(dy, w, *, K=None, out=None, residual=None, gate=None, gate_scale=1.0,
+                 out_f32=None, accumulate=False):
+    """dx = dy @ w: dy [M,N_out], w [N_out, K_in] -> [M, K_in]."""
+    M = dy.shape[0]
+    Kc = K if K is not None else w.shape[0]
+    Nin = w.shape[1]
+    if out is None and out_f32 is None:
+        out = torch.empty(M, Nin, device=dy.device, dtype=dy.dtype)
+    gemm(dy, w, M=M, N=Nin, K=Kc, a_kcontig=True, b_kcontig=False, out=out, out_f32=out_f32,
+         accumulate=accumulate, residual=residual, gate=gate, gate_scale=gate_scale,
+         dtype=dy.dtype)
+    return out if out is not None else out_f32
+
+
+def linear_wgrad(dy, x, dw, *, M=None, accumulate=True):
+    """dw (+)= dy^T @ x: dy [T, M_out(ld)], x [T, K_in] -> dw fp32 [M_out, K_in]."""
+    T = dy.shape[0]
+    Mo = M if M is not None else dy.shape[1]
+    gemm(dy, x, M=Mo, N=x.shape[1], K=T, a_kcontig=False, b_kcontig=False, out_f32=dw,
+         accumulate=accumulate, dtype=dy.dtype)
+
+
+# ---------------------------------------------------------------------------
+def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale, drop_p=0.0,
+             seed=0):
+    call("smer_attn_fwd", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k),
+         _p(v), _ld(v), _p(o), _ld(o), _p(lse), _p(kpm), int(causal), float(scale),
+         float(drop_p), int(seed) & 0xFFFFFFFF, _stream())
+
+
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, causal=False,
+             scale, drop_p=0.0, seed=0):
+    lib = load()
+    dt = dtype_code(q.dtype)
+    nbytes = lib.smer_attn_bwd_workspace(dt, B, H, Lq, Lk)
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=q.device)
+    call("smer_attn_bwd", dt, B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v),
+         _p(o), _ld(o), _p(do), _ld(do), _p(lse), _p(kpm), int(causal), float(scale),
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(dq), _ld(dq), _p(dk), _ld(dk), _p(dv),
+         _ld(dv), _p(ws), nbytes, _stream())
+
+
+def attn_weights(q, k, lse, out, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale):
+    call("smer_attn_weights", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k),
+         _ld(k), _p(lse), _p(kpm), int(causal), float(scale), _p(out), _stream())
+
+
+def attn_decode(q, kcache, vcache, row_req, row_nkeys, out, *, H, D, row_stride, req_stride,
+                scale):
+    call("smer_attn_decode", dtype_code(q.dtype), q.shape[0], H, D, _p(q), _ld(q), _p(kcache),
+         _p(vcache), int(row_stride), int(req_stride), _p(row_req), _p(row_nkeys), _p(out),
+         _ld(out), float(scale), _stream())
+
+
+def kv_scatter(src, cache, row_req, row_pos, *, row_stride, req_stride):
+    call("smer_kv_scatter", dtype_code(src.dtype), src.shape[0], src.shape[1], _p(src), _ld(src),
+         _p(cache), int(row_stride), int(req_stride), _p(row_req), _p(row_pos), _stream())
+
+
+# ---------------------------------------------------------------------------
+def layernorm(x, gamma, beta, y, mean, rstd, eps=1e-5):
+    M, N = x.shape
+    call("smer_layernorm_fwd", dtype_code(x.dtype), M, N, _p(x), _ld(x), _p(gamma), _p(beta),
+         float(eps), _p(y), _ld(y), _p(mean), _p(rstd), _stream())
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dx, *, dx_drop=None, drop_p=0.0, seed=0,
+                  dgamma=None, dbeta=None, accumulate=True):
+    lib = load()
+    M, N = x.shape
+    nbytes = lib.smer_layernorm_bwd_workspace(M, N) if (dgamma is not None or dbeta is not None) else 0
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=x.device)
+    call("smer_layernorm_bwd", dtype_code(x.dtype), M, N, _p(dy), _ld(dy),
+         int(dy.dtype == torch.float32 and x.dtype != torch.float32), _p(x), _ld(x), _p(mean),
+         _p(rstd), _p(gamma), _p(dx), _ld(dx), _p(dx_drop),
+         _ld(dx_drop) if dx_drop is not None else 0, float(drop_p), int(seed) & 0xFFFFFFFF,
+         _p(dgamma), _p(dbeta), int(accumulate), _p(ws), nbytes, _stream())
+
+
+def embed(ids, table, pe, out, *, L=0, positions=None, scale, drop_p=0.0, seed=0):
+    n_tok = ids.numel()
+    d = table.shape[1]
+    call("smer_embed_fwd", dtype_code(out.dtype), n_tok, d, _p(ids), _p(positions), int(L),
+         _p(table), _p(pe), float(scale), float(drop_p), int(seed) & 0xFFFFFFFF, _p(out),
+         _ld(out), _stream())
+
+
+def embed_bwd(dtable, scale, segs):
+    """segs: list of up to two (ids int64 [n], dx [n, d], drop_p, seed)."""
+    lib = load()
+    V, d = dtable.shape
+    segs = list(segs) + [(None, None, 0.0, 0)] * (2 - len(segs))
+    (i0, x0, p0, s0), (i1, x1, p1, s1) = segs
+    n0 = i0.numel() if i0 is not None else 0
+    n1 = i1.numel() if i1 is not None else 0
+    dt = dtype_code((x0 if x0 is not None else x1).dtype)
+    nbytes = lib.smer_embed_bwd_workspace(V, d, n0 + n1)
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dtable.device)
+    call("smer_embed_bwd", dt, V, d, float(scale), _p(i0), _p(x0),
+         _ld(x0) if x0 is not None else 0, n0, float(p0), int(s0) & 0xFFFFFFFF, _p(i1), _p(x1),
+         _ld(x1) if x1 is not None else 0, n1, float(p1), int(s1) & 0xFFFFFFFF, _p(dtable),
+         _p(ws), nbytes, _stream())
+
+
+def wce_denom(y, ce_all, denom):
+    call("smer_wce_denom", y.numel(), _p(y), _p(ce_all), _p(denom), _stream())
+
+
+def wce_fwd_bwd(logits, y, w, denom, row_loss, loss_out=None, dlogits=None, *, V=None,
+                grad_scale=1.0):
+    R = logits.shape[0]
+    Vv = V if V is not None else logits.shape[1]
+    dt = dtype_code(dlogits.dtype) if dlogits is not None else F32
+    call("smer_wce_fwd_bwd", dt, R, Vv, _p(logits), _ld(logits), _p(y), _p(w), _p(denom),
+         _p(row_loss), _p(loss_out), _p(dlogits), _ld(dlogits) if dlogits is not None else 0,
+         float(grad_scale), _stream())
+
+
+def adam(p, g, m, v, p_bf16, *, lr, b1, b2, eps, step):
+    import math
+    bc1 = 1.0 - b1 ** step
+    bc2s = math.sqrt(1.0 - b2 ** step)
+    call("smer_adam", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), float(lr), float(b1),
+         float(b2), float(eps), float(bc1), float(bc2s), _stream())
+
+
+def cast(src, dst):
+    assert src.numel() == dst.numel()
+    call("smer_cast", dtype_code(src.dtype), dtype_code(dst.dtype), src.numel(), _p(src),
+         _p(dst), _stream())
+
+
+def colsum(x, out, *, N=None, accumulate=True):
+    lib = load()
+    M = x.shape[0]
+    Nn = N if N is not None else x.shape[1]
+    nbytes = lib.smer_colsum_workspace(M, Nn)
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=x.device)
+    call("smer_colsum", dtype_code(x.dtype), M, Nn, _p(x), _ld(x), _p(out), int(accumulate),
+         _p(ws), nbytes, _stream())
