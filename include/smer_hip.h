@@ -146,6 +146,9 @@ int smer_adam(long n, float* p, const float* g, float* m, float* v, void* p_bf16
 
 int smer_cast(int src_dtype, int dst_dtype, long n, const void* src, void* dst,
               smer_stream_t stream);
+/* strided 2-D copy with dtype conversion (dst[r*ldd+c] = src[r*lds+c]). */
+int smer_cast2d(int src_dtype, int dst_dtype, int rows, int cols, const void* src, long lds,
+                void* dst, long ldd, smer_stream_t stream);
 size_t smer_colsum_workspace(int M, int N);
 /* out[n] (+)= sum_m x[m, n] (deterministic two-stage). */
 int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, int accumulate,

@@ -52,6 +52,7 @@ SIGNATURES = {
     "smer_adam": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float,
                           c_float, P]),
     "smer_cast": (c_int, [c_int, c_int, c_long, P, P, P]),
+    "smer_cast2d": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P]),
     "smer_colsum_workspace": (c_size, [c_int, c_int]),
     "smer_colsum": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, P, c_size, P]),
 }

@@ -186,6 +186,35 @@ extern "C" int smer_cast(int src_dtype, int dst_dtype, long n, const void* src, 
   return SMER_OK;
 }
 
+template <typename S, typename D>
+__global__ void cast2d_kernel(int rows, int cols, const S* __restrict__ s, long lds,
+                              D* __restrict__ d, long ldd) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)rows * cols) return;
+  int r = idx / cols, c = idx % cols;
+  d[(long)r * ldd + c] = from_f32<D>(to_f32(s[(long)r * lds + c]));
+}
+
+extern "C" int smer_cast2d(int src_dtype, int dst_dtype, int rows, int cols, const void* src,
+                           long lds, void* dst, long ldd, smer_stream_t stream) {
+  long n = (long)rows * cols;
+  if (n == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g((n + 255) / 256);
+  if (src_dtype == SMER_F32 && dst_dtype == SMER_BF16)
+    hipLaunchKernelGGL((cast2d_kernel<float, bf16>), g, dim3(256), 0, s, rows, cols, (const float*)src, lds, (bf16*)dst, ldd);
+  else if (src_dtype == SMER_F32 && dst_dtype == SMER_F32)
+    hipLaunchKernelGGL((cast2d_kernel<float, float>), g, dim3(256), 0, s, rows, cols, (const float*)src, lds, (float*)dst, ldd);
+  else if (src_dtype == SMER_BF16 && dst_dtype == SMER_F32)
+    hipLaunchKernelGGL((cast2d_kernel<bf16, float>), g, dim3(256), 0, s, rows, cols, (const bf16*)src, lds, (float*)dst, ldd);
+  else if (src_dtype == SMER_BF16 && dst_dtype == SMER_BF16)
+    hipLaunchKernelGGL((cast2d_kernel<bf16, bf16>), g, dim3(256), 0, s, rows, cols, (const bf16*)src, lds, (bf16*)dst, ldd);
+  else
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_cast2d: dtype");
+  SMER_CHECK_LAUNCH("smer_cast2d");
+  return SMER_OK;
+}
+
 extern "C" size_t smer_colsum_workspace(int M, int N) {
   return (size_t)((M + CS_ROWS - 1) / CS_ROWS) * N * sizeof(float);
 }

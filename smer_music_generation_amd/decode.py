@@ -1,0 +1,156 @@
+"""KV-cached, batched incremental decoder for the infill loop.
+
+The reference re-runs the whole encoder over S source tokens and the whole
+decoder over the t-token prefix for EVERY generated token
+(`generation.py:542-545` -> `model_generate`, `generation.py:209-225`).
+Here, per request:
+  * prefill: the encoder runs once; every decoder layer's cross-attention
+    K/V of the memory (`transformer.py:463`) is computed once into a cache;
+  * step: only the new token(s) go through the decoder; their self-attention
+    K/V are appended to a per-layer cache that persists ACROSS spans (the
+    prefix accumulates, `generation.py:686`), positions continue.
+Mathematically identical to the full recompute (causal attention: earlier
+positions never see later tokens); fp32 mode reproduces the reference logits
+to ~1e-6 and its greedy token ids exactly.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+class DecodeSession:
+    def __init__(self, model, max_requests, max_src, max_tgt, precision=None):
+        if precision is not None:
+            model.set_precision(precision)
+        self.model = model
+        self.eng = model.engine
+        eng = self.eng
+        self.dt = eng.act_dtype()
+        dev = model.flat_parameters().device
+        if not dev.type == "cuda":
+            raise RuntimeError("DecodeSession needs the model on a ROCm GPU")
+        self.dev = dev
+        self.R, self.Smax, self.Tmax = int(max_requests), int(max_src), int(max_tgt)
+        d = eng.d
+        self.d = d
+        if max(self.Smax, self.Tmax) > model.pos_enc.pe.shape[0]:
+            model.pos_enc.extend(max(self.Smax, self.Tmax))
+        self.self_kv = [torch.zeros(self.R, self.Tmax, 2 * d, dtype=self.dt, device=dev)
+                        for _ in range(eng.n_dec)]
+        self.cross_kv = [torch.zeros(self.R, self.Smax, 2 * d, dtype=self.dt, device=dev)
+                         for _ in range(eng.n_dec)]
+        self.src_len = np.zeros(self.R, dtype=np.int64)
+        self.W = eng.weights(self.dt)
+
+    def refresh_weights(self):
+        self.W = self.eng.weights(self.dt)
+
+    # ------------------------------------------------------------------
+    def prefill(self, slots, srcs):
+        """Encode `srcs` (list of 1-D int arrays) into request `slots`."""
+        eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
+        H, D = eng.H, eng.D
+        B = len(slots)
+        lens = [len(s) for s in srcs]
+        S = max(lens)
+        if S > self.Smax:
+            raise ValueError("source length %d exceeds session max_src %d" % (S, self.Smax))
+        src = np.zeros((B, S), dtype=np.int64)
+        for b, s in enumerate(srcs):
+            src[b, :len(s)] = np.asarray(s, dtype=np.int64)
+        src_t = torch.from_numpy(src).to(dev)
+        kpm = None
+        if min(lens) != S:
+            kpm = torch.from_numpy((np.arange(S)[None, :] >= np.array(lens)[:, None]).astype(np.uint8)).to(dev)
+        pe = self.model.pos_enc.pe
+        pe2 = pe.view(pe.shape[0], pe.shape[2])
+        x = torch.empty(B * S, d, dtype=dt, device=dev)
+        ops.embed(src_t.view(-1), W.emb, pe2, x, L=S, scale=math.sqrt(d))
+        scale = 1.0 / math.sqrt(D)
+        for L in W.enc:
+            qkv = ops.linear(x, L.in_w, L.in_b)
+            o = torch.empty(B * S, d, dtype=dt, device=dev)
+            lse = torch.empty(B, H, S, device=dev)
+            ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S,
+                         Lk=S, D=D, kpm=kpm, causal=False, scale=scale)
+            y1 = ops.linear(o, L.out_w, L.out_b, residual=x)
+            x1, _, _ = eng._ln(y1, L.n1, dt)
+            h = ops.linear(x1, L.l1_w, L.l1_b, relu=True)
+            y2 = ops.linear(h, L.l2_w, L.l2_b, residual=x1)
+            x, _, _ = eng._ln(y2, L.n2, dt)
+        mem, _, _ = eng._ln(x, W.enc_norm, dt)
+        # scatter the valid memory rows' cross K/V into the per-request caches
+        rows_b = np.concatenate([np.full(n, slots[b], dtype=np.int32) for b, n in enumerate(lens)])
+        rows_j = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        rows_src = np.concatenate([b * S + np.arange(n) for b, n in enumerate(lens)])
+        sel = torch.from_numpy(rows_src.astype(np.int64)).to(dev)
+        req_t = torch.from_numpy(rows_b).to(dev)
+        pos_t = torch.from_numpy(rows_j).to(dev)
+        mem_rows = mem if min(lens) == S else mem.index_select(0, sel)
+        for li, L in enumerate(W.dec):
+            kvc = ops.linear(mem_rows, L.ckv_w, L.ckv_b)
+            ops.kv_scatter(kvc, self.cross_kv[li], req_t, pos_t, row_stride=2 * d,
+                           req_stride=self.Smax * 2 * d)
+        for b, s in enumerate(slots):
+            self.src_len[s] = lens[b]
+
+    # ------------------------------------------------------------------
+    def step(self, feeds):
+        """feeds: list of (slot, new_token_ids, first_position).  Returns fp32
+        logits [len(feeds), V] (numpy) of each feed's LAST new token."""
+        eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
+        H, D = eng.H, eng.D
+        ids, pos, req, last = [], [], [], []
+        for slot, toks, p0 in feeds:
+            n = len(toks)
+            if p0 + n > self.Tmax:
+                raise ValueError("decoder prefix exceeds session max_tgt %d" % self.Tmax)
+            ids.extend(int(t) for t in toks)
+            pos.extend(range(p0, p0 + n))
+            req.extend([slot] * n)
+            last.append(len(ids) - 1)
+        M = len(ids)
+        meta = np.empty((4, M), dtype=np.int32)
+        meta[0] = pos
+        meta[1] = req
+        meta[2] = meta[0] + 1
+        meta[3] = self.src_len[meta[1]]
+        meta_t = torch.from_numpy(meta).to(dev, non_blocking=False)
+        ids_t = torch.tensor(ids, dtype=torch.int64, device=dev)
+        pos_t, req_t, nks_t, nkc_t = meta_t[0], meta_t[1], meta_t[2], meta_t[3]
+        pe = self.model.pos_enc.pe
+        pe2 = pe.view(pe.shape[0], pe.shape[2])
+        x = torch.empty(M, d, dtype=dt, device=dev)
+        ops.embed(ids_t, W.emb, pe2, x, positions=pos_t, scale=math.sqrt(d))
+        scale = 1.0 / math.sqrt(D)
+        sstride = self.Tmax * 2 * d
+        cstride = self.Smax * 2 * d
+        for li, L in enumerate(W.dec):
+            qkv = ops.linear(x, L.sa_w, L.sa_b)
+            cache = self.self_kv[li]
+            ops.kv_scatter(qkv[:, d:], cache, req_t, pos_t, row_stride=2 * d, req_stride=sstride)
+            o = torch.empty(M, d, dtype=dt, device=dev)
+            ops.attn_decode(qkv[:, :d], cache, cache.view(-1)[d:], req_t, nks_t, o, H=H, D=D,
+                            row_stride=2 * d, req_stride=sstride, scale=scale)
+            y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=x)
+            x1, _, _ = eng._ln(y1, L.n1, dt)
+            qc = ops.linear(x1, L.cq_w, L.cq_b)
+            cc = self.cross_kv[li]
+            oc = torch.empty(M, d, dtype=dt, device=dev)
+            ops.attn_decode(qc, cc, cc.view(-1)[d:], req_t, nkc_t, oc, H=H, D=D,
+                            row_stride=2 * d, req_stride=cstride, scale=scale)
+            y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
+            x2, _, _ = eng._ln(y2, L.n2, dt)
+            h = ops.linear(x2, L.l1_w, L.l1_b, relu=True)
+            y3 = ops.linear(h, L.l2_w, L.l2_b, residual=x2)
+            x, _, _ = eng._ln(y3, L.n3, dt)
+        out, _, _ = eng._ln(x, W.dec_norm, dt)
+        logits = torch.empty(M, eng.V, device=dev)
+        ops.gemm(out, W.fc_w, M=M, N=eng.V, K=d, out_f32=logits, bias=W.fc_b, dtype=dt)
+        lg = logits.cpu().numpy()
+        return lg[last]

@@ -1,0 +1,435 @@
+"""Forward / backward schedule of the SMER encoder-decoder on gfx950 kernels.
+
+Layout: activations are batch-major token rows [B*L, d] (row = b*L + i)
+instead of the reference's seq-first [L, B, d] — the per-token math of
+`transformer.py:378-470` is unchanged, only the row order differs, and
+rows of one sequence are contiguous for the attention tiles.
+
+Every op is a libsmer_hip.so call (see ops.py); torch provides tensors
+(memory), the stream and autograd plumbing only.
+
+Per encoder layer (transformer.py:389-395):
+    qkv = x Wqkv^T + b                       smer_gemm
+    o   = softmax(q k^T / sqrt(dh) + kpm) v  smer_attn_fwd   (dropout on P)
+    y1  = x + drop(o Wo^T + bo)              smer_gemm (residual + dropout epilogue)
+    x1  = LN1(y1)                            smer_layernorm_fwd
+    h   = drop(relu(x1 W1^T + b1))           smer_gemm
+    y2  = x1 + drop(h W2^T + b2)             smer_gemm
+    x2  = LN2(y2)
+Decoder layers add the causal self-attention and the cross-attention
+(transformer.py:459-469); the final norms and the vocab head follow
+(transformer.py:274-275, 329-330, model.py:106).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+
+_SITE = {"pe_src": 1, "pe_tgt": 2}
+
+
+def _site(kind, layer, which):
+    return 16 + (layer * 16 + which) * 2 + (0 if kind == "enc" else 1)
+
+
+class _W:
+    pass
+
+
+class Engine:
+    def __init__(self, model):
+        self.m = model
+        self.d = model.d_model
+        self.H = model.nhead
+        self.D = self.d // self.H
+        self.F = model.dim_feedforward
+        self.V = model.vocab_size
+        self.Vp = (self.V + 63) // 64 * 64
+        self.n_enc = model.num_encoder_layers
+        self.n_dec = model.num_decoder_layers
+        self._bf16 = None
+        self._bf16_version = None
+        self._fc_pad = None
+
+    # ------------------------------------------------------------------
+    def act_dtype(self):
+        return torch.bfloat16 if self.m.precision == "bf16" else torch.float32
+
+    def _weights_flat(self, dt):
+        flat = self.m.flat_parameters()
+        if dt == torch.float32:
+            return flat
+        ver = self._version_key()
+        if self._bf16 is None or self._bf16.numel() != flat.numel() or self._bf16_version != ver:
+            if self._bf16 is None or self._bf16.numel() != flat.numel():
+                self._bf16 = torch.empty(flat.numel(), dtype=torch.bfloat16, device=flat.device)
+            ops.cast(flat, self._bf16)
+            self._fc_pad = None
+            self._bf16_version = ver
+        return self._bf16
+
+    def _version_key(self):
+        # parameters are .data-views of the flat buffer; in-place updates by
+        # any optimizer bump the per-parameter version counters
+        flat = self.m.flat_parameters()
+        return (flat.data_ptr(), flat._version, sum(p._version for p in self.m.parameters()))
+
+    def mark_bf16_fresh(self):
+        """Called by the fused Adam, which rewrites the bf16 copy itself."""
+        self._bf16_version = self._version_key()
+        self._fc_pad = None
+
+    def weights(self, dt):
+        """Per-layer views of the working weights (bf16 copy or fp32 master);
+        biases / norms always fp32 master."""
+        work = self._weights_flat(dt)
+        master = self.m.flat_parameters()
+        off = self.m._offsets
+        d, F, V = self.d, self.F, self.V
+
+        def wv(name, shape):
+            o = off[name]
+            return work[o: o + math.prod(shape)].view(shape)
+
+        def mv(name, n):
+            o = off[name]
+            return master[o: o + n]
+
+        W = _W()
+        W.emb = mv("embedding.weight", V * d).view(V, d)
+        W.enc, W.dec = [], []
+        for i in range(self.n_enc):
+            p = "transformer.encoder.layers.%d" % i
+            L = _W()
+            L.in_w, L.in_b = wv(p + ".self_attn.in_proj_weight", (3 * d, d)), mv(p + ".self_attn.in_proj_bias", 3 * d)
+            L.out_w, L.out_b = wv(p + ".self_attn.out_proj.weight", (d, d)), mv(p + ".self_attn.out_proj.bias", d)
+            L.l1_w, L.l1_b = wv(p + ".linear1.weight", (F, d)), mv(p + ".linear1.bias", F)
+            L.l2_w, L.l2_b = wv(p + ".linear2.weight", (d, F)), mv(p + ".linear2.bias", d)
+            L.n1 = (mv(p + ".norm1.weight", d), mv(p + ".norm1.bias", d))
+            L.n2 = (mv(p + ".norm2.weight", d), mv(p + ".norm2.bias", d))
+            W.enc.append(L)
+        W.enc_norm = (mv("transformer.encoder.norm.weight", d), mv("transformer.encoder.norm.bias", d))
+        for i in range(self.n_dec):
+            p = "transformer.decoder.layers.%d" % i
+            L = _W()
+            L.sa_w, L.sa_b = wv(p + ".self_attn.in_proj_weight", (3 * d, d)), mv(p + ".self_attn.in_proj_bias", 3 * d)
+            L.sa_ow, L.sa_ob = wv(p + ".self_attn.out_proj.weight", (d, d)), mv(p + ".self_attn.out_proj.bias", d)
+            ca = wv(p + ".multihead_attn.in_proj_weight", (3 * d, d))
+            cb = mv(p + ".multihead_attn.in_proj_bias", 3 * d)
+            L.cq_w, L.cq_b, L.ckv_w, L.ckv_b = ca[:d], cb[:d], ca[d:], cb[d:]
+            L.ca_ow, L.ca_ob = wv(p + ".multihead_attn.out_proj.weight", (d, d)), mv(p + ".multihead_attn.out_proj.bias", d)
+            L.l1_w, L.l1_b = wv(p + ".linear1.weight", (F, d)), mv(p + ".linear1.bias", F)
+            L.l2_w, L.l2_b = wv(p + ".linear2.weight", (d, F)), mv(p + ".linear2.bias", d)
+            L.n1 = (mv(p + ".norm1.weight", d), mv(p + ".norm1.bias", d))
+            L.n2 = (mv(p + ".norm2.weight", d), mv(p + ".norm2.bias", d))
+            L.n3 = (mv(p + ".norm3.weight", d), mv(p + ".norm3.bias", d))
+            W.dec.append(L)
+        W.dec_norm = (mv("transformer.decoder.norm.weight", d), mv("transformer.decoder.norm.bias", d))
+        W.fc_w = wv("fc.weight", (V, d))
+        W.fc_b = mv("fc.bias", V)
+        # vocab head padded to Vp rows (zero rows) for the K = V dgrad
+        if self._fc_pad is None or self._fc_pad.dtype != dt or self._fc_pad.device != work.device:
+            self._fc_pad = torch.zeros(self.Vp, d, dtype=dt, device=work.device)
+        ops.cast(W.fc_w.reshape(-1), self._fc_pad[:V].reshape(-1))
+        W.fc_pad = self._fc_pad
+        return W
+
+    def grad_views(self):
+        g = self.m.flat_grad()
+        off = self.m._offsets
+        d, F, V = self.d, self.F, self.V
+
+        def gv(name, shape):
+            o = off[name]
+            return g[o: o + math.prod(shape)].view(shape)
+
+        G = _W()
+        G.emb = gv("embedding.weight", (V, d))
+        G.enc, G.dec = [], []
+        for i in range(self.n_enc):
+            p = "transformer.encoder.layers.%d" % i
+            L = _W()
+            L.in_w, L.in_b = gv(p + ".self_attn.in_proj_weight", (3 * d, d)), gv(p + ".self_attn.in_proj_bias", (3 * d,))
+            L.out_w, L.out_b = gv(p + ".self_attn.out_proj.weight", (d, d)), gv(p + ".self_attn.out_proj.bias", (d,))
+            L.l1_w, L.l1_b = gv(p + ".linear1.weight", (F, d)), gv(p + ".linear1.bias", (F,))
+            L.l2_w, L.l2_b = gv(p + ".linear2.weight", (d, F)), gv(p + ".linear2.bias", (d,))
+            L.n1 = (gv(p + ".norm1.weight", (d,)), gv(p + ".norm1.bias", (d,)))
+            L.n2 = (gv(p + ".norm2.weight", (d,)), gv(p + ".norm2.bias", (d,)))
+            G.enc.append(L)
+        G.enc_norm = (gv("transformer.encoder.norm.weight", (d,)), gv("transformer.encoder.norm.bias", (d,)))
+        for i in range(self.n_dec):
+            p = "transformer.decoder.layers.%d" % i
+            L = _W()
+            L.sa_w, L.sa_b = gv(p + ".self_attn.in_proj_weight", (3 * d, d)), gv(p + ".self_attn.in_proj_bias", (3 * d,))
+            L.sa_ow, L.sa_ob = gv(p + ".self_attn.out_proj.weight", (d, d)), gv(p + ".self_attn.out_proj.bias", (d,))
+            ca = gv(p + ".multihead_attn.in_proj_weight", (3 * d, d))
+            cb = gv(p + ".multihead_attn.in_proj_bias", (3 * d,))
+            L.cq_w, L.cq_b, L.ckv_w, L.ckv_b = ca[:d], cb[:d], ca[d:], cb[d:]
+            L.ca_ow, L.ca_ob = gv(p + ".multihead_attn.out_proj.weight", (d, d)), gv(p + ".multihead_attn.out_proj.bias", (d,))
+            L.l1_w, L.l1_b = gv(p + ".linear1.weight", (F, d)), gv(p + ".linear1.bias", (F,))
+            L.l2_w, L.l2_b = gv(p + ".linear2.weight", (d, F)), gv(p + ".linear2.bias", (d,))
+            L.n1 = (gv(p + ".norm1.weight", (d,)), gv(p + ".norm1.bias", (d,)))
+            L.n2 = (gv(p + ".norm2.weight", (d,)), gv(p + ".norm2.bias", (d,)))
+            L.n3 = (gv(p + ".norm3.weight", (d,)), gv(p + ".norm3.bias", (d,)))
+            G.dec.append(L)
+        G.dec_norm = (gv("transformer.decoder.norm.weight", (d,)), gv("transformer.decoder.norm.bias", (d,)))
+        G.fc_w = gv("fc.weight", (V, d))
+        G.fc_b = gv("fc.bias", (V,))
+        return G
+
+    # ------------------------------------------------------------------
+    def _ln(self, x, wb, dt):
+        M = x.shape[0]
+        y = torch.empty_like(x)
+        mean = torch.empty(M, device=x.device)
+        rstd = torch.empty(M, device=x.device)
+        ops.layernorm(x, wb[0], wb[1], y, mean, rstd)
+        return y, mean, rstd
+
+    def forward(self, src, tgt, src_kpm, tgt_kpm, mem_kpm, *, training, need_weights, save,
+                seed=0):
+        """Returns (logits fp32 [B*T, V], weights [L,B,T,S] or None, ctx)."""
+        m = self.m
+        dt = self.act_dtype()
+        dev = src.device
+        B, S = src.shape
+        T = tgt.shape[1]
+        d, H, D = self.d, self.H, self.D
+        scale = 1.0 / math.sqrt(D)
+        p_pos = float(m.pos_dropout) if training else 0.0
+        p_tr = float(m.trans_dropout) if training else 0.0
+        W = self.weights(dt)
+        pe = m.pos_enc.pe
+        if max(S, T) > pe.shape[0]:
+            raise RuntimeError("sequence length %d exceeds max_seq_length %d" % (max(S, T), pe.shape[0]))
+        pe2 = pe.view(pe.shape[0], pe.shape[2])
+        src_ids = src.reshape(-1).contiguous().long()
+        tgt_ids = tgt.reshape(-1).contiguous().long()
+        skpm = src_kpm.to(torch.uint8).contiguous() if src_kpm is not None else None
+        tkpm = tgt_kpm.to(torch.uint8).contiguous() if tgt_kpm is not None else None
+        mkpm = mem_kpm.to(torch.uint8).contiguous() if mem_kpm is not None else None
+        sd = lambda site: (seed * 1000003 + site) & 0xFFFFFFFF  # noqa: E731
+        ctx = _W()
+        ctx.B, ctx.S, ctx.T, ctx.dt, ctx.p_pos, ctx.p_tr, ctx.seed = B, S, T, dt, p_pos, p_tr, seed
+        ctx.src_ids, ctx.tgt_ids, ctx.skpm, ctx.tkpm, ctx.mkpm = src_ids, tgt_ids, skpm, tkpm, mkpm
+        ctx.enc, ctx.dec = [], []
+
+        x = torch.empty(B * S, d, dtype=dt, device=dev)
+        ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
+        for i, L in enumerate(W.enc):
+            qkv = ops.linear(x, L.in_w, L.in_b)
+            o = torch.empty(B * S, d, dtype=dt, device=dev)
+            lse = torch.empty(B, H, S, device=dev)
+            ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
+                         D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)))
+            y1 = ops.linear(o, L.out_w, L.out_b, residual=x, drop_p=p_tr, seed=sd(_site("enc", i, 1)))
+            x1, m1, r1 = self._ln(y1, L.n1, dt)
+            h = ops.linear(x1, L.l1_w, L.l1_b, relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
+            y2 = ops.linear(h, L.l2_w, L.l2_b, residual=x1, drop_p=p_tr, seed=sd(_site("enc", i, 3)))
+            x2, m2, r2 = self._ln(y2, L.n2, dt)
+            if save:
+                ctx.enc.append((x, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2))
+            x = x2
+        mem, me, re = self._ln(x, W.enc_norm, dt)
+        ctx.enc_last = (x, me, re)
+        ctx.mem = mem
+
+        y = torch.empty(B * T, d, dtype=dt, device=dev)
+        ops.embed(tgt_ids, W.emb, pe2, y, L=T, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_tgt"]))
+        wts = torch.empty(self.n_dec, B, T, S, device=dev) if need_weights else None
+        for i, L in enumerate(W.dec):
+            qkv = ops.linear(y, L.sa_w, L.sa_b)
+            o = torch.empty(B * T, d, dtype=dt, device=dev)
+            lse = torch.empty(B, H, T, device=dev)
+            ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
+                         D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)))
+            y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr, seed=sd(_site("dec", i, 1)))
+            x1, m1, r1 = self._ln(y1, L.n1, dt)
+            qc = ops.linear(x1, L.cq_w, L.cq_b)
+            kvc = ops.linear(mem, L.ckv_w, L.ckv_b)
+            oc = torch.empty(B * T, d, dtype=dt, device=dev)
+            lsec = torch.empty(B, H, T, device=dev)
+            ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
+                         causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)))
+            if need_weights:
+                ops.attn_weights(qc, kvc[:, :d], lsec, wts[i], B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
+                                 scale=scale)
+            y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1, drop_p=p_tr, seed=sd(_site("dec", i, 3)))
+            x2, m2, r2 = self._ln(y2, L.n2, dt)
+            h = ops.linear(x2, L.l1_w, L.l1_b, relu=True, drop_p=p_tr, seed=sd(_site("dec", i, 4)))
+            y3 = ops.linear(h, L.l2_w, L.l2_b, residual=x2, drop_p=p_tr, seed=sd(_site("dec", i, 5)))
+            x3, m3, r3 = self._ln(y3, L.n3, dt)
+            if save:
+                ctx.dec.append((y, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2,
+                                h, y3, m3, r3))
+            y = x3
+        out, mo, ro = self._ln(y, W.dec_norm, dt)
+        ctx.dec_last = (y, mo, ro)
+        ctx.dec_out = out
+        logits = torch.empty(B * T, self.V, device=dev)
+        ops.gemm(out, W.fc_w, M=B * T, N=self.V, K=d, out_f32=logits, bias=W.fc_b, dtype=dt)
+        return logits, wts, ctx
+
+    # ------------------------------------------------------------------
+    def backward(self, ctx, dlog_pad, hook=None):
+        """dlog_pad: [B*T, Vp] activation dtype (cols >= V zero).  Accumulates
+        every parameter gradient into the flat grad buffer.  `hook(name)` is
+        called after each layer's grads are final (DP bucket overlap)."""
+        m = self.m
+        dt = ctx.dt
+        dev = dlog_pad.device
+        B, S, T = ctx.B, ctx.S, ctx.T
+        d, H, D, V = self.d, self.H, self.D, self.V
+        scale = 1.0 / math.sqrt(D)
+        p_tr = ctx.p_tr
+        sd = lambda site: (ctx.seed * 1000003 + site) & 0xFFFFFFFF  # noqa: E731
+        W = self.weights(dt)
+        G = self.grad_views()
+        Mt, Ms = B * T, B * S
+
+        # vocab head
+        g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
+        ops.linear_wgrad(dlog_pad, ctx.dec_out, G.fc_w, M=V)
+        ops.colsum(dlog_pad, G.fc_b, N=V)
+        # final decoder norm
+        y_last, mo, ro = ctx.dec_last
+        dy = torch.empty_like(y_last)
+        ops.layernorm_bwd(g_out, y_last, mo, ro, W.dec_norm[0], dy, dgamma=G.dec_norm[0],
+                          dbeta=G.dec_norm[1])
+        if hook:
+            hook("head")
+        dmem = torch.zeros(Ms, d, device=dev)
+        for i in reversed(range(self.n_dec)):
+            L, GL = W.dec[i], G.dec[i]
+            (y_in, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2, h, y3, m3,
+             r3) = ctx.dec[i]
+            # FFN block: x3 = LN3(x2 + drop(W2 drop(relu(W1 x2))))
+            dy3 = torch.empty_like(y3)
+            dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
+            ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
+                              drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1])
+            dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=1.0 / (1.0 - p_tr))
+            ops.linear_wgrad(dy3d, h, GL.l2_w)
+            ops.colsum(dy3d, GL.l2_b)
+            dx2 = ops.linear_dgrad(dh, L.l1_w, residual=dy3)
+            ops.linear_wgrad(dh, x2, GL.l1_w)
+            ops.colsum(dh, GL.l1_b)
+            # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
+            dy2 = torch.empty_like(y2)
+            dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
+            ops.layernorm_bwd(dx2, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
+                              drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+            doc = ops.linear_dgrad(dy2d, L.ca_ow)
+            ops.linear_wgrad(dy2d, oc, GL.ca_ow)
+            ops.colsum(dy2d, GL.ca_ob)
+            dqc = torch.empty(Mt, d, dtype=dt, device=dev)
+            dkvc = torch.empty(Ms, 2 * d, dtype=dt, device=dev)
+            ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
+                         B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
+                         drop_p=p_tr, seed=sd(_site("dec", i, 2)))
+            dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
+            ops.linear_wgrad(dqc, x1, GL.cq_w)
+            ops.colsum(dqc, GL.cq_b)
+            ops.linear_dgrad(dkvc, L.ckv_w, out_f32=dmem, accumulate=True)
+            ops.linear_wgrad(dkvc, ctx.mem, GL.ckv_w)
+            ops.colsum(dkvc, GL.ckv_b)
+            # self-attention block
+            dy1 = torch.empty_like(y1)
+            dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
+            ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
+                              drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+            do = ops.linear_dgrad(dy1d, L.sa_ow)
+            ops.linear_wgrad(dy1d, o, GL.sa_ow)
+            ops.colsum(dy1d, GL.sa_ob)
+            dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
+            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
+                         dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
+                         kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
+                         seed=sd(_site("dec", i, 0)))
+            dy = ops.linear_dgrad(dqkv, L.sa_w, residual=dy1)
+            ops.linear_wgrad(dqkv, y_in, GL.sa_w)
+            ops.colsum(dqkv, GL.sa_b)
+            if hook:
+                hook("dec%d" % i)
+        d_tgt = dy
+        # encoder
+        x_last, me, re = ctx.enc_last
+        dx = torch.empty_like(x_last)
+        ops.layernorm_bwd(dmem, x_last, me, re, W.enc_norm[0], dx, dgamma=G.enc_norm[0],
+                          dbeta=G.enc_norm[1])
+        for i in reversed(range(self.n_enc)):
+            L, GL = W.enc[i], G.enc[i]
+            (x_in, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2) = ctx.enc[i]
+            dy2 = torch.empty_like(y2)
+            dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
+            ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
+                              drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+            dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=1.0 / (1.0 - p_tr))
+            ops.linear_wgrad(dy2d, h, GL.l2_w)
+            ops.colsum(dy2d, GL.l2_b)
+            dx1 = ops.linear_dgrad(dh, L.l1_w, residual=dy2)
+            ops.linear_wgrad(dh, x1, GL.l1_w)
+            ops.colsum(dh, GL.l1_b)
+            dy1 = torch.empty_like(y1)
+            dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
+            ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
+                              drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+            do = ops.linear_dgrad(dy1d, L.out_w)
+            ops.linear_wgrad(dy1d, o, GL.out_w)
+            ops.colsum(dy1d, GL.out_b)
+            dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
+            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
+                         dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
+                         kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
+                         seed=sd(_site("enc", i, 0)))
+            dx = ops.linear_dgrad(dqkv, L.in_w, residual=dy1)
+            ops.linear_wgrad(dqkv, x_in, GL.in_w)
+            ops.colsum(dqkv, GL.in_b)
+            if hook:
+                hook("enc%d" % i)
+        # shared embedding (model.py:76): both streams scatter into one table
+        ops.embed_bwd(G.emb, math.sqrt(d), [(ctx.src_ids, dx, ctx.p_pos, sd(_SITE["pe_src"])),
+                                            (ctx.tgt_ids, d_tgt, ctx.p_pos, sd(_SITE["pe_tgt"]))])
+        if hook:
+            hook("embedding")
+
+
+# ----------------------------------------------------------------------
+# autograd entry used by ScoreTransformer.forward
+# ----------------------------------------------------------------------
+class ScoreTransformerFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(fctx, anchor, model, src, tgt, src_kpm, tgt_kpm, mem_kpm, tgt_mask):
+        eng = model.engine
+        if not src.is_cuda:
+            raise RuntimeError("the SMER engine runs on the GPU: move the model and inputs to "
+                               "a ROCm device first")
+        training = model.training and (model.pos_dropout > 0 or model.trans_dropout > 0)
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
+        need_grad = torch.is_grad_enabled() and anchor.requires_grad
+        logits, wts, ctx = eng.forward(src, tgt, src_kpm, tgt_kpm, mem_kpm,
+                                       training=model.training, need_weights=model.need_weights,
+                                       save=need_grad, seed=seed)
+        fctx.eng = eng
+        fctx.ctx = ctx
+        fctx.model = model
+        B, T = tgt.shape
+        out = logits.view(B, T, eng.V)
+        w = wts.permute(1, 0, 2, 3) if wts is not None else None
+        if w is not None:
+            fctx.mark_non_differentiable(w)
+        return out, w
+
+    @staticmethod
+    def backward(fctx, dlogits, dweights):
+        eng = fctx.eng
+        ctx = fctx.ctx
+        B, T = ctx.B, ctx.T
+        dl = torch.zeros(B * T, eng.Vp, dtype=ctx.dt, device=dlogits.device)
+        ops.cast2d(dlogits.reshape(B * T, eng.V).contiguous().float(), dl, cols=eng.V)
+        eng.backward(ctx, dl)
+        fctx.ctx = None
+        return (None,) * 8

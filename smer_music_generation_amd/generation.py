@@ -1,0 +1,332 @@
+"""Infill call surface of the plugin (reference `generation.py`).
+
+Same names, signatures, return values and error behaviour as the
+reference: `model_generate` (209-225), `generation_all` (468-696),
+`sampling` (41-95), `softmax_with_temperature` (28-30), `weighted_sampling`
+(33-38), `nucleus` (11-25), `gen_nopeek_mask` (193-206), plus the wire
+helpers (`mask_bar_and_track`, `restore_marked_input`, `fill_empty_bars`,
+`change_controls`) and the north-star alias `infill = generation_all`.
+
+Differences, all opt-in keywords with reference defaults:
+  * `generation_all(..., use_kv_cache=True)`: decode through the KV-cached
+    `DecodeSession` (one encoder pass per request) instead of re-running the
+    full model per token; `use_kv_cache=False` is the reference algorithm.
+  * `greedy=False`: True replaces `weighted_sampling` by argmax.
+  * `generation_batch(...)`: many requests decoded in lockstep.
+The grammar state machine, the -100 logit masking, the float64 softmax and
+the numpy RNG consumption are the reference's, so with the same
+`np.random` state the same token ids come out.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .decode import DecodeSession
+from .durations import durations_for_events
+from .wire import (change_controls, fill_empty_bars, mask_bar_and_track,  # noqa: F401
+                   mask_targets, restore_marked_input)
+
+
+# --------------------------------------------------------------------------
+# sampling (generation.py:11-95)
+# --------------------------------------------------------------------------
+def nucleus(probs, p):
+    probs /= (sum(probs) + 1e-5)
+    sorted_probs = np.sort(probs)[::-1]
+    sorted_index = np.argsort(probs)[::-1]
+    csum = np.cumsum(sorted_probs)
+    after = csum > p
+    if sum(after) > 0:
+        cand = sorted_index[:np.where(after)[0][0] + 1]
+    else:
+        cand = sorted_index[:]
+    cp = np.array([probs[i] for i in cand])
+    cp /= sum(cp)
+    return np.random.choice(cand, size=1, p=cp)[0]
+
+
+def softmax_with_temperature(logits, temperature):
+    e = np.exp(logits / temperature)
+    return e / np.sum(e)
+
+
+def weighted_sampling(probs):
+    probs /= sum(probs)
+    sorted_probs = np.sort(probs)[::-1]
+    sorted_index = np.argsort(probs)[::-1]
+    return np.random.choice(sorted_index, size=1, p=sorted_probs)[0]
+
+
+_FLAG_NAMES = ("no_pitch", "no_duration", "no_rest", "no_whole_duration", "no_eos",
+               "no_continue", "no_sep", "is_density", "is_polyphony", "is_occupation",
+               "is_tensile", "no_control")
+_MASK_CACHE = {}
+
+
+def allowed_ids(vocab, **flags):
+    """Boolean [V]: logits `sampling` keeps (others become -100).  The
+    reference's `no_control` test (`i in dict.values()`) never matches
+    (SURVEY Q1), so it is a no-op here too."""
+    key = (id(vocab),) + tuple(bool(flags.get(f, False)) for f in _FLAG_NAMES)
+    hit = _MASK_CACHE.get(key)
+    if hit is not None:
+        return hit
+    V = vocab.vocab_size
+    keep = np.ones(V, dtype=bool)
+    g = flags.get
+    if g("no_pitch"):
+        keep[vocab.pitch_indices] = False
+    if g("no_duration"):
+        keep[vocab.duration_only_indices] = False
+    if g("no_continue"):
+        keep[vocab.continue_index] = False
+    if g("no_rest"):
+        keep[vocab.rest_indices] = False
+    if g("no_sep"):
+        keep[vocab.sep_indices] = False
+    if g("no_whole_duration"):
+        keep[vocab.duration_only_indices[0]] = False
+    if g("no_eos"):
+        keep[vocab.eos_index] = False
+    for flag, attr in (("is_density", "density_indices"), ("is_occupation", "occupation_indices"),
+                       ("is_polyphony", "polyphony_indices"), ("is_tensile", "tensile_indices")):
+        if g(flag):
+            only = np.zeros(V, dtype=bool)
+            only[getattr(vocab, attr)] = True
+            keep &= only
+    keep[vocab.program_indices + vocab.structure_indices + vocab.time_signature_indices +
+         vocab.tempo_indices] = False
+    keep.setflags(write=False)
+    _MASK_CACHE[key] = keep
+    return keep
+
+
+def sampling(logit, vocab, p=None, t=1.0, greedy=False, **flags):
+    """`generation.py:41-95` with vectorised masking."""
+    if isinstance(logit, torch.Tensor):
+        logit = logit.squeeze().detach().cpu().numpy()
+    lg = np.where(allowed_ids(vocab, **flags), np.asarray(logit, dtype=np.float32).astype(np.float64),
+                  -100.0)
+    probs = softmax_with_temperature(lg, t)
+    if greedy:
+        return int(np.argmax(probs))
+    if p is not None:
+        return nucleus(probs, p)
+    return weighted_sampling(probs)
+
+
+def gen_nopeek_mask(length):
+    m = (torch.triu(torch.ones(length, length)) == 1).transpose(0, 1)
+    return m.float().masked_fill(m == 0, float("-inf")).masked_fill(m == 1, 0.0)
+
+
+def model_generate(model, src, tgt, device, return_weights=False):
+    """`generation.py:209-225`: batch-1 full forward; logits [t, V] on CPU."""
+    src = torch.as_tensor(src).clone().detach().unsqueeze(0).long().to(device)
+    tgt = torch.tensor(tgt).unsqueeze(0).to(device)
+    mask = gen_nopeek_mask(tgt.shape[1]).unsqueeze(0).to(device)
+    with torch.no_grad():
+        out, w = model.forward(src, tgt, src_key_padding_mask=None, tgt_key_padding_mask=None,
+                               memory_key_padding_mask=None, tgt_mask=mask)
+    if return_weights:
+        return out.squeeze(0).to("cpu"), (w.squeeze(0).to("cpu") if w is not None else None)
+    return out.squeeze(0).to("cpu")
+
+
+# --------------------------------------------------------------------------
+# the per-span grammar state machine (generation.py:528-687)
+# --------------------------------------------------------------------------
+class _Span:
+    """Decoding state of one request: mask index, span tokens, grammar flags."""
+
+    def __init__(self, vocab, src, mask_target, all_controls, no_whole, greedy, logger):
+        self.v = vocab
+        self.src = src
+        self.mask_target = mask_target
+        self.all_controls = set(int(c) for c in all_controls)
+        self.no_whole = no_whole
+        self.greedy = greedy
+        self.logger = logger
+        self.m0 = vocab.char2index('m_0')
+        self.eos = vocab.char2index('<eos>')
+        self.n_masks = int(np.sum(np.asarray(src) == self.m0))
+        self.mask_idx = 0
+        self.tgt_inp = []
+        self.total = []
+        self.done = self.n_masks == 0
+        self._start_span()
+
+    def _start_span(self):
+        self.this_in = [self.m0]
+        self.this_ev = ['m_0']
+        self.in_pitch = self.in_rest = self.in_sep = self.in_continue = False
+
+    def prefix(self):
+        return self.tgt_inp + self.this_in
+
+    def _draw(self, logit, check, failmsg, **flags):
+        idx = sampling(logit, self.v, greedy=self.greedy, **flags)
+        if check is None:
+            return idx
+        n = 0
+        while check(idx):
+            idx = sampling(logit, self.v, greedy=self.greedy, **flags)
+            n += 1
+            if n > 10:
+                if self.logger is not None:
+                    self.logger.info(failmsg)
+                break
+        return idx
+
+    def advance(self, logit):
+        """Consume the logits of the current prefix's last position."""
+        v = self.v
+        if self.in_sep:
+            idx = self._draw(logit, lambda i: i in v.rest_indices or i == v.eos_index or
+                             i == v.duration_only_indices[0], "in sep failed", no_rest=True,
+                             no_sep=True, no_eos=True, no_whole_duration=True, no_control=True)
+        elif self.in_continue:
+            idx = self._draw(logit, lambda i: i not in v.pitch_indices, 'in continue failed',
+                             no_rest=True, no_sep=True, no_duration=True, no_continue=True,
+                             no_eos=True, no_control=True)
+        elif self.in_pitch:
+            idx = self._draw(logit, lambda i: i not in v.duration_only_indices and
+                             i not in v.pitch_indices, 'in pitch failed', no_rest=True,
+                             no_sep=True, no_continue=True, no_whole_duration=self.no_whole,
+                             no_eos=True, no_control=True)
+        elif self.in_rest:
+            idx = self._draw(logit, lambda i: i not in v.duration_only_indices, 'in rest failed',
+                             no_pitch=True, no_rest=True, no_sep=True, no_continue=True,
+                             no_whole_duration=self.no_whole, no_eos=True, no_control=True)
+        elif len(self.this_in) == 1:
+            tc = self.mask_target[self.mask_idx]
+            if tc != 'r':
+                flag = {'d': 'is_density', 'o': 'is_occupation', 'p': 'is_polyphony'}.get(tc, 'is_tensile')
+                idx = self._draw(logit, None, '', **{flag: True})
+            else:
+                idx = self._draw(logit, lambda i: i in v.duration_only_indices, 'start failed',
+                                 no_duration=True, no_control=True)
+        else:
+            idx = self._draw(logit, None, '', no_whole_duration=self.no_whole, no_control=True)
+        idx = int(idx)
+        ev = v.index2char(idx)
+        if idx == v.continue_index:
+            self.in_continue, self.in_sep = True, False
+        if idx in v.pitch_indices:
+            self.in_pitch, self.in_sep, self.in_continue = True, False, False
+        if idx in v.duration_only_indices:
+            self.in_rest, self.in_pitch = False, False
+        if ev == 'sep':
+            self.in_sep = True
+        if ev == 'rest':
+            self.in_rest = True
+        if idx in self.all_controls:
+            self.this_in += [idx, self.eos]
+            self.this_ev += [ev, '<eos>']
+        else:
+            self.this_in.append(idx)
+            self.this_ev.append(ev)
+        if self.this_in[-1] == self.eos or len(self.this_in) >= 100:
+            self.tgt_inp.extend(self.this_in[:-1])
+            self.total.extend(self.this_ev[:-1])
+            self.mask_idx += 1
+            if self.mask_idx >= self.n_masks:
+                self.done = True
+            else:
+                self._start_span()
+        return idx
+
+
+def _prepare(events, vocab, tracks_to_generate, bars_to_generate):
+    """generation.py:470-516: duration tables, mask targets, masked src."""
+    name_to_time, time_to_name, times, bar_duration = durations_for_events(events)
+    n_bars = sum(1 for e in events if e == 'bar')
+    target, tracks = mask_targets(events, tracks_to_generate, bars_to_generate)
+    if bars_to_generate[-1] >= n_bars:
+        events = fill_empty_bars(events, bars_to_generate[-1] - n_bars + 1, bar_duration,
+                                 time_to_name, times)
+    src, mtn, mbn = mask_bar_and_track(events, vocab, tracks, bars_to_generate)
+    no_whole = not (int(events[0][0]) >= 4 and int(events[0][2]) == 4)
+    return src, mtn, mbn, target, no_whole
+
+
+def generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
+                   bars_to_generate, *, greedy=False, use_kv_cache=True):
+    """`generation.py:468-696`.  Returns (restored '<U9' tokens,
+    mask_track_names, mask_bar_names) or None (nothing masked / on error,
+    after printing it, as the reference does)."""
+    try:
+        src, mtn, mbn, target, no_whole = _prepare(events, vocab, tracks_to_generate,
+                                                   bars_to_generate)
+        st = _Span(vocab, src, target, all_controls, no_whole, greedy, logger)
+        if st.n_masks == 0:
+            return None
+        model.eval()
+        with torch.no_grad():
+            if use_kv_cache:
+                sess = DecodeSession(model, 1, len(src), max(128, 100 * st.n_masks + 8))
+                sess.prefill([0], [src])
+                fed = 0
+                while not st.done:
+                    pre = st.prefix()
+                    logit = sess.step([(0, pre[fed:], fed)])[0]
+                    fed = len(pre)
+                    st.advance(logit)
+            else:
+                src_t = torch.tensor(src)
+                while not st.done:
+                    out = model_generate(model, src_t, st.prefix(), device)
+                    st.advance(out[-1].numpy())
+        src_token = [vocab.index2char(int(t)) for t in src]
+        return restore_marked_input(src_token, st.total), mtn, mbn
+    except Exception as e:  # reference behaviour (generation.py:695-696)
+        print(e)
+
+
+infill = generation_all
+
+
+def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logger=None,
+                     max_tgt=None, precision=None, return_stats=False):
+    """Decode many infill requests in lockstep on one KV-cached session.
+
+    requests: list of (events, tracks_to_generate, bars_to_generate).
+    Returns a list of (restored, mask_track_names, mask_bar_names) (None
+    where nothing was masked), and optionally {'tokens', 'steps'}."""
+    preps = [_prepare(list(ev), vocab, tr, br) for ev, tr, br in requests]
+    spans = [_Span(vocab, p[0], p[3], all_controls, p[4], greedy, logger) for p in preps]
+    R = len(requests)
+    Smax = max(len(p[0]) for p in preps)
+    Tmax = max_tgt or max(128, 100 * max(s.n_masks for s in spans) + 8)
+    model.eval()
+    tokens = steps = 0
+    with torch.no_grad():
+        sess = DecodeSession(model, R, Smax, Tmax, precision=precision)
+        sess.prefill(list(range(R)), [p[0] for p in preps])
+        fed = [0] * R
+        while True:
+            live = [i for i in range(R) if not spans[i].done]
+            if not live:
+                break
+            feeds = []
+            for i in live:
+                pre = spans[i].prefix()
+                feeds.append((i, pre[fed[i]:], fed[i]))
+                fed[i] = len(pre)
+            lg = sess.step(feeds)
+            for k, i in enumerate(live):
+                before = len(spans[i].tgt_inp) + len(spans[i].this_in)
+                spans[i].advance(lg[k])
+                tokens += 1
+            steps += 1
+    out = []
+    for p, st in zip(preps, spans):
+        if st.n_masks == 0:
+            out.append(None)
+            continue
+        src_token = [vocab.index2char(int(t)) for t in p[0]]
+        out.append((restore_marked_input(src_token, st.total), p[1], p[2]))
+    if return_stats:
+        return out, {"tokens": tokens, "steps": steps}
+    return out

@@ -199,6 +199,13 @@ def cast(src, dst):
          _p(dst), _stream())
 
 
+def cast2d(src, dst, *, rows=None, cols=None):
+    r = rows if rows is not None else src.shape[0]
+    c = cols if cols is not None else src.shape[1]
+    call("smer_cast2d", dtype_code(src.dtype), dtype_code(dst.dtype), r, c, _p(src), _ld(src),
+         _p(dst), _ld(dst), _stream())
+
+
 def colsum(x, out, *, N=None, accumulate=True):
     lib = load()
     M = x.shape[0]
