@@ -1,0 +1,251 @@
+"""Headline benchmark: SMER train tokens/s (+ infill tokens/s) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-infill] [--no-cpu]
+
+Workload (BASELINE.json configs[1] / SURVEY.md §8d C2): 6-layer encoder +
+6-layer decoder, d_model 512, 8 heads, FF 2048, V 309, per GPU B=32 source
+sequences of S=1024 SMER tokens and T=256 decoder tokens (synthetic SMER
+grammar, seeded), bf16 MFMA compute with fp32 master weights, dropout 0.1
+as the reference trains (train.py:257-259), the full step timed: forward,
+fused weighted CE, backward, RCCL gradient all-reduce (N>1), Adam.
+One step = one pass over one batch.  value = N*B*(S+T)*K / max-rank time.
+
+Infill (second block, replicas only): batched greedy KV-cached decode of
+32 requests per GPU on the same model with S~1024 sources.
+
+Multi-GPU: launched by torch.distributed.run, one rank per GPU, RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CTRL = ['key', 'tensile', 'density', 'polyphony', 'occupation']
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
+
+
+def train_flops_per_sample(L, d, F, V, S, T):
+    """forward algorithmic flops per sample (attention dense)."""
+    enc = L * (8 * S * d * d + 4 * S * d * F + 4 * S * S * d)
+    dec = L * (12 * T * d * d + 4 * T * T * d + 4 * S * d * d + 4 * T * S * d + 4 * T * d * F)
+    return enc + dec + 2 * T * d * V
+
+
+def make_model(args, dev, precision="bf16"):
+    from smer_music_generation_amd.model import ScoreTransformer
+    torch.manual_seed(0)
+    m = ScoreTransformer(309, args.d_model, args.nhead, args.layers, args.layers, args.ff, 2400,
+                         args.dropout, args.dropout, precision=precision)
+    for p in m.parameters():  # train.py:261-263
+        if p.dim() > 1:
+            torch.nn.init.xavier_normal_(p)
+    return m.to(dev)
+
+
+def bench_train(args, dev, rank, world):
+    from smer_music_generation_amd import ops
+    from smer_music_generation_amd.synth import synth_training_batch
+    from smer_music_generation_amd.train import Trainer
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, CTRL)
+    m = make_model(args, dev)
+    tr = Trainer(m, v, lr=1e-4)
+    b = synth_training_batch(1000 + rank, v, args.batch, args.seq, args.tgt)
+    bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
+    for _ in range(args.warmup):
+        tr.step(bt)
+    torch.cuda.synchronize()
+    timer = ops.KernelTimer() if args.roofline else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.GEMM_TIMER = timer
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = tr.step(bt)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ops.GEMM_TIMER = None
+    dt = t1 - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    tokens = world * args.batch * (args.seq + args.tgt) * args.steps
+    flops_sample = train_flops_per_sample(args.layers, args.d_model, args.ff, 309, args.seq, args.tgt)
+    step_flops = 3.0 * flops_sample * args.batch  # per GPU: fwd + 2x bwd
+    res = {"tokens_per_s": tokens / dt, "ms_per_step": 1000 * dt / args.steps,
+           "tgt_tokens_per_s": world * args.batch * args.tgt * args.steps / dt,
+           "loss": float(loss.item()),
+           "step_tflops_per_gpu": step_flops / (dt / args.steps) / 1e12,
+           "mfma_frac_whole_step": step_flops / (dt / args.steps) / 1e12 / BF16_PEAK_TFLOPS}
+    if timer is not None:
+        s = timer.summary()
+        achieved = s["flops"] / (s["total_ms"] / 1e3) / 1e12
+        res["gemm"] = {"launches": s["launches"], "avg_us": 1000 * s["total_ms"] / max(1, s["launches"]),
+                       "flops_per_launch": s["flops"] / max(1, s["launches"]),
+                       "tflops": achieved, "share_of_step": s["total_ms"] / (1000 * dt)}
+    return res
+
+
+def _infill_requests(n, target_len=1024, seed0=0):
+    from smer_music_generation_amd.synth import synth_events
+    reqs = []
+    for i in range(n):
+        nb = 8
+        ev = synth_events(seed0 + i, n_bars=nb, n_tracks=3)
+        while len(ev) < target_len - 120:
+            nb += 2
+            ev = synth_events(seed0 + i, n_bars=nb, n_tracks=3)
+        reqs.append((ev, [i % 3], [nb - 4, nb - 3]))
+    return reqs
+
+
+def bench_infill(args, dev, rank):
+    from smer_music_generation_amd.generation import generation_batch
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, CTRL)
+    m = make_model(args, dev).eval()
+    all_controls = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
+    warm = _infill_requests(4, args.seq, 900)
+    generation_batch(m, warm, v, all_controls, greedy=True)
+    reqs = _infill_requests(args.infill_batch, args.seq, 100 * rank)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    _, st = generation_batch(m, reqs, v, all_controls, greedy=True, return_stats=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    src_len = float(np.mean([len(r[0]) for r in reqs]))
+    return {"tokens": st["tokens"], "steps": st["steps"], "seconds": dt,
+            "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len}
+
+
+def cpu_baseline(args):
+    """The oracle (torch-CPU fp32 restatement of the reference step) on a
+    bounded sample of the same workload: B=2 sequences of the C2 shape."""
+    from oracle import ref_cpu
+    from smer_music_generation_amd.synth import synth_training_batch
+    from smer_music_generation_amd.vocab import WordVocab
+    threads = os.cpu_count() or 1
+    threads = min(threads, 16)
+    torch.set_num_threads(threads)
+    v = WordVocab(0, CTRL)
+    cfg = dict(d_model=args.d_model, nhead=args.nhead, num_encoder_layers=args.layers,
+               num_decoder_layers=args.layers)
+    sd = ref_cpu.init_params(309, args.d_model, args.ff, args.layers, args.layers, seed=0)
+    sd["pos_enc.pe"] = ref_cpu.pe_table(2400, args.d_model)
+    B = 2
+    b = synth_training_batch(7, v, B, args.seq, args.tgt)
+    ref_cpu.train_step(sd, cfg, b, v.control_indices, 0.8, 8)  # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        ref_cpu.train_step(sd, cfg, b, v.control_indices, 0.8, 8)
+        n += 1
+        if time.perf_counter() - t0 > 10.0 or n >= 5:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": B * (args.seq + args.tgt) * n / dt, "unit": "tokens/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d oracle train steps (fwd+bwd, fp32, torch CPU) at B=%d S=%d T=%d, C2 model"
+                      % (n, B, args.seq, args.tgt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--tgt", type=int, default=256)
+    ap.add_argument("--layers", type=int, default=6)
+    ap.add_argument("--d-model", dest="d_model", type=int, default=512)
+    ap.add_argument("--nhead", type=int, default=8)
+    ap.add_argument("--ff", type=int, default=2048)
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--infill-batch", dest="infill_batch", type=int, default=32)
+    ap.add_argument("--no-infill", dest="infill", action="store_false")
+    ap.add_argument("--no-cpu", dest="cpu", action="store_false")
+    ap.add_argument("--no-roofline", dest="roofline", action="store_false")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from smer_music_generation_amd import _lib
+    _lib.load()
+
+    tr = bench_train(args, dev, rank, world)
+    inf = None
+    if args.infill:
+        inf = bench_infill(args, dev, rank)
+        if world > 1:
+            t = torch.tensor([inf["tokens"], inf["seconds"]], device=dev, dtype=torch.float64)
+            tok = t[0:1].clone()
+            dist.all_reduce(tok)
+            sec = t[1:2].clone()
+            dist.all_reduce(sec, op=dist.ReduceOp.MAX)
+            inf["tokens_per_s"] = tok.item() / sec.item()
+    cpu = cpu_baseline(args) if (args.cpu and rank == 0 and world == 1) else None
+
+    if rank == 0:
+        roof = None
+        if "gemm" in tr:
+            g = tr["gemm"]
+            roof = {"bound": "mfma", "kernel": "gemm_bf16_kernel (smer_gemm)",
+                    "achieved": round(g["tflops"], 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(g["tflops"] / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "avg_launch_us": round(g["avg_us"], 2),
+                    "flops_per_launch": g["flops_per_launch"],
+                    "share_of_step_time": round(g["share_of_step"], 3)}
+        line = {
+            "metric": "infill tokens/sec + train tokens/sec, SMER seq_len=1024, 1/2/4/8 MI355X",
+            "value": round(tr["tokens_per_s"], 1), "unit": "train tokens/s (B*(S+T))",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tr["ms_per_step"], 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic SMER-grammar token batches (seeded), random xavier_normal weights",
+            "config": {"workload": "C2 train step: 6+6 layers d512 h8 ff2048 V309, per-GPU "
+                                   "B=%d S=%d T=%d, dropout %.1f, fused WCE + Adam%s"
+                                   % (args.batch, args.seq, args.tgt, args.dropout,
+                                      " + RCCL grad all-reduce" if world > 1 else ""),
+                       "global_batch": args.batch * world, "seq_len": args.seq,
+                       "tgt_len": args.tgt, "parallelism": "dp%d" % world},
+            "train": {k: (round(val, 4) if isinstance(val, float) else val)
+                      for k, val in tr.items() if k != "gemm"},
+            "roofline": roof,
+            "infill": inf and {"metric": "infill tokens/s (greedy, KV-cached, batched)",
+                               "value": round(inf["tokens_per_s"], 1),
+                               "requests_per_gpu": inf["requests"],
+                               "mean_src_len": round(inf["mean_src_len"], 1),
+                               "decode_steps": inf["steps"], "tokens": inf["tokens"],
+                               "parallelism": "replicas"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

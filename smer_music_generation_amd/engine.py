@@ -402,14 +402,13 @@ class Engine:
 # ----------------------------------------------------------------------
 class ScoreTransformerFunction(torch.autograd.Function):
     @staticmethod
-    def forward(fctx, anchor, model, src, tgt, src_kpm, tgt_kpm, mem_kpm, tgt_mask):
+    def forward(fctx, anchor, model, need_grad, src, tgt, src_kpm, tgt_kpm, mem_kpm, tgt_mask):
         eng = model.engine
         if not src.is_cuda:
             raise RuntimeError("the SMER engine runs on the GPU: move the model and inputs to "
                                "a ROCm device first")
         training = model.training and (model.pos_dropout > 0 or model.trans_dropout > 0)
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if training else 0
-        need_grad = torch.is_grad_enabled() and anchor.requires_grad
         logits, wts, ctx = eng.forward(src, tgt, src_kpm, tgt_kpm, mem_kpm,
                                        training=model.training, need_weights=model.need_weights,
                                        save=need_grad, seed=seed)
@@ -432,4 +431,4 @@ class ScoreTransformerFunction(torch.autograd.Function):
         ops.cast2d(dlogits.reshape(B * T, eng.V).contiguous().float(), dl, cols=eng.V)
         eng.backward(ctx, dl)
         fctx.ctx = None
-        return (None,) * 8
+        return (None,) * 9

@@ -299,6 +299,7 @@ class ScoreTransformer(nn.Module):
         mask (`train.py:1356-1369`); only tgt_mask[0] is used (`model.py:95`)."""
         if src.size(0) != tgt.size(0):
             raise RuntimeError("the batch number of src and tgt must be equal")
+        need_grad = torch.is_grad_enabled() and self.embedding.weight.requires_grad
         return _engine.ScoreTransformerFunction.apply(
-            self.embedding.weight, self, src, tgt, src_key_padding_mask, tgt_key_padding_mask,
+            self.embedding.weight, self, need_grad, src, tgt, src_key_padding_mask, tgt_key_padding_mask,
             memory_key_padding_mask, tgt_mask)

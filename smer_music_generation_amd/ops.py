@@ -42,11 +42,42 @@ def _ld(t):
 
 
 # ---------------------------------------------------------------------------
+class KernelTimer:
+    """Optional live timing of GEMM launches with HIP events on the launch
+    stream (bench.py roofline): records (start, end, flops) per launch."""
+
+    def __init__(self):
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        ms = [s.elapsed_time(e) for s, e, _ in self.records]
+        fl = [f for _, _, f in self.records]
+        return {"launches": len(ms), "total_ms": float(sum(ms)), "flops": float(sum(fl))}
+
+
+GEMM_TIMER = None  # set to a KernelTimer to instrument smer_gemm launches
+
+
 def gemm(A, B, *, M, N, K, a_kcontig=True, b_kcontig=True, out=None, out_f32=None,
          accumulate=False, bias=None, alpha=1.0, relu=False, residual=None, gate=None,
          gate_scale=1.0, drop_p=0.0, seed=0, dtype=None):
     """out (+)= epilogue(alpha * op(A) op(B)^T); see include/smer_hip.h."""
     dt = dtype_code(dtype if dtype is not None else A.dtype)
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _gemm_call(dt, A, B, M, N, K, a_kcontig, b_kcontig, out, out_f32, accumulate, bias, alpha,
+               relu, residual, gate, gate_scale, drop_p, seed)
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * K))
+
+
+def _gemm_call(dt, A, B, M, N, K, a_kcontig, b_kcontig, out, out_f32, accumulate, bias, alpha,
+               relu, residual, gate, gate_scale, drop_p, seed):
     call("smer_gemm", dt, int(a_kcontig), int(b_kcontig), M, N, K, _p(A), _ld(A), _p(B), _ld(B),
          _p(bias), float(alpha), int(relu), _p(residual),
          _ld(residual) if residual is not None else 0, _p(gate),
