@@ -61,7 +61,10 @@ const char* smer_last_error(void);
  * epilogue(v) = residual + dropout(relu?(v + bias))  then  *gate-mask,
  *   gate (nullable, [M,N] ld ldg): v *= (gate > 0 ? gate_scale : 0)
  * outputs: C (activation dtype, nullable) and/or Cf (fp32, nullable;
- *   accumulate=1 adds into Cf).  bf16 path: MFMA 16x16x32; f32 path: VALU. */
+ *   accumulate=1 adds into Cf).  bf16 path: MFMA 16x16x32; f32 path: VALU.
+ * workspace (nullable, 16-B aligned): lets a Cf-only GEMM with few output
+ *   tiles and a long K (weight gradients) split K into deterministic fp32
+ *   slabs of M*N floats each, summed in fixed order by a second kernel. */
 int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
               const void* A, long lda, const void* B, long ldb,
               const float* bias, float alpha, int relu,
@@ -69,7 +72,7 @@ int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
               const void* gate, long ldg, float gate_scale,
               float drop_p, uint32_t drop_seed,
               void* C, long ldc, float* Cf, long ldcf, int accumulate,
-              smer_stream_t stream);
+              void* workspace, size_t ws_bytes, smer_stream_t stream);
 
 /* Flash attention over [B*L, *] token-row layouts (row = b*L + i), head h
  * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:

@@ -427,10 +427,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
   }
 }
 
-// delta[bh, i] = sum_d dO[i, h*D + d] * O[i, h*D + d]
 template <typename T>
-__global__ void attn_delta(int B, int H, int Lq, int D, const T* __restrict__ o, long ldo,
-                           const T* __restrict__ dout, long lddo, float* __restrict__ delta) {
+__global__ void attn_delta_scalar(int B, int H, int Lq, int D, const T* __restrict__ o, long ldo,
+                                  const T* __restrict__ dout, long lddo, float* __restrict__ delta) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)B * H * Lq;
   if (idx >= total) return;
@@ -442,6 +441,52 @@ __global__ void attn_delta(int B, int H, int Lq, int D, const T* __restrict__ o,
   float s = 0.f;
   for (int d = 0; d < D; ++d) s += to_f32(orow[d]) * to_f32(drow[d]);
   delta[idx] = s;
+}
+
+// delta[bh, i] = sum_d dO[i, h*D + d] * O[i, h*D + d]
+// LPR = D/8 lanes per (row, head), 8 elements (one 16-B bf16 load) per lane.
+template <typename T, int LPR>
+__global__ __launch_bounds__(256) void attn_delta(int B, int H, int Lq, int D,
+                                                  const T* __restrict__ o, long ldo,
+                                                  const T* __restrict__ dout, long lddo,
+                                                  float* __restrict__ delta) {
+  const long item = ((long)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int part = threadIdx.x % LPR;
+  const long total = (long)B * H * Lq;
+  const bool ok = item < total;
+  float s = 0.f;
+  if (ok) {
+    int i = item % Lq;
+    int bh = item / Lq;
+    int b = bh / H, h = bh % H;
+    float a[8], c[8];
+    load8<T>(o + (long)(b * Lq + i) * ldo + h * D + part * 8, 8, a);
+    load8<T>(dout + (long)(b * Lq + i) * lddo + h * D + part * 8, 8, c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += a[k] * c[k];
+  }
+#pragma unroll
+  for (int off = 1; off < LPR; off <<= 1) s += __shfl_xor(s, off, 64);
+  if (ok && part == 0) {
+    int i = item % Lq;
+    int bh = item / Lq;
+    delta[(long)bh * Lq + i] = s;
+  }
+}
+
+template <typename T>
+static void launch_delta(int B, int H, int Lq, int D, const void* o, long ldo, const void* dout,
+                         long lddo, float* delta, hipStream_t s) {
+  long threads = (long)B * H * Lq * (D / 8);
+  dim3 g((threads + 255) / 256);
+  if (D == 32)
+    hipLaunchKernelGGL((attn_delta<T, 4>), g, dim3(256), 0, s, B, H, Lq, D, (const T*)o, ldo, (const T*)dout, lddo, delta);
+  else if (D == 64)
+    hipLaunchKernelGGL((attn_delta<T, 8>), g, dim3(256), 0, s, B, H, Lq, D, (const T*)o, ldo, (const T*)dout, lddo, delta);
+  else if (D == 128)
+    hipLaunchKernelGGL((attn_delta<T, 16>), g, dim3(256), 0, s, B, H, Lq, D, (const T*)o, ldo, (const T*)dout, lddo, delta);
+  else
+    hipLaunchKernelGGL((attn_delta_scalar<T>), dim3(((long)B * H * Lq + 255) / 256), dim3(256), 0, s, B, H, Lq, D, (const T*)o, ldo, (const T*)dout, lddo, delta);
 }
 
 // ---------------------------------------------------------------------------
@@ -760,15 +805,15 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   long nrow = (long)B * H * Lq;
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v) && al16(dout), "smer_attn_bwd: 16-B alignment");
-    hipLaunchKernelGGL(attn_delta<bf16>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H, Lq, D,
-                       (const bf16*)o, ldo, (const bf16*)dout, lddo, delta);
+    SMER_REQUIRE(al16(o) && ldo % 8 == 0 && lddo % 8 == 0, "smer_attn_bwd: O/dO alignment");
+    launch_delta<bf16>(B, H, Lq, D, o, ldo, dout, lddo, delta, s);
     if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
     else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
     else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
-    hipLaunchKernelGGL(attn_delta<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H, Lq, D,
-                       (const float*)o, ldo, (const float*)dout, lddo, delta);
+    hipLaunchKernelGGL(attn_delta_scalar<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H,
+                       Lq, D, (const float*)o, ldo, (const float*)dout, lddo, delta);
     size_t doff = ((size_t)nrow * sizeof(float) + 255) & ~(size_t)255;
     float* ws_p = (float*)((char*)workspace + doff);
     float* ws_s = ws_p + (size_t)B * H * Lq * Lk;

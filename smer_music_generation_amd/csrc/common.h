@@ -59,6 +59,30 @@ static inline uint32_t smer_drop_threshold(float p) {
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
+// out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order.
+// Workgroup = 64 columns x 4 partial-row groups; deterministic.
+__global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const float* __restrict__ part,
+                                                       long stride, long off, float* __restrict__ out,
+                                                       int accumulate, float scale);
+
+// Load 8 consecutive elements as floats (16-B vector when aligned & in range).
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
+  if (valid >= 8) {
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (float)r[i];
+    } else {
+      float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = i < valid ? (float)p[i] : 0.f;
+  }
+}
+
 __device__ __forceinline__ bf16x8 lds_read_b128(const char* base, uint32_t byte_off) {
   return *reinterpret_cast<const bf16x8*>(base + byte_off);
 }

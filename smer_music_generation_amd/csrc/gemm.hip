@@ -11,6 +11,8 @@
 // f32 path (parity mode): LDS-tiled VALU FMA, same epilogue.
 #include "common.h"
 
+#include <algorithm>
+
 struct GemmEpi {
   const float* bias;
   float alpha;
@@ -119,17 +121,21 @@ template <bool AK, bool BKC>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
                                                            const bf16* __restrict__ A, long lda,
                                                            const bf16* __restrict__ B, long ldb,
-                                                           GemmEpi e) {
+                                                           GemmEpi e, int ksplit, int kchunk,
+                                                           float* __restrict__ slabs) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = (M + GBM - 1) / GBM, nbn = (N + GBN - 1) / GBN;
-  const int nwg = nbm * nbn;
-  // bijective XCD remap (blocks b and b+8 share an XCD): give each XCD a
-  // contiguous run of tiles, then walk tiles in GM-row groups for L2 reuse.
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int nwg = nbm * nbn * ksplit;
+  // Bijective XCD remap (blocks b and b+8 share an XCD): each XCD gets a
+  // contiguous run of work items; the K slices of one tile are adjacent
+  // (same XCD), tiles are walked in GM-row groups for L2 reuse.
+  const int braw = blockIdx.x;
+  const int xcd = braw & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (braw >> 3);
+  const int split = lin % ksplit;
+  const int wgid = lin / ksplit;
   constexpr int GM = 8;
   const int grp = wgid / (GM * nbn);
   const int first_m = grp * GM;
@@ -137,8 +143,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   const int within = wgid % (GM * nbn);
   const int tm = first_m + within % gsz, tn = within / gsz;
   const int m0 = tm * GBM, n0 = tn * GBN;
-
-  // buffer b: A at smem + b*2*TILE_BYTES, B right after it
+  const int k_begin = split * kchunk;
+  const int k_end = min(K, k_begin + kchunk);
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -147,9 +153,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[4], rb[4];
-  const int nk = (K + GBK - 1) / GBK;
-  stage_load<AK>(ra, A, lda, M, K, m0, 0, tid);
-  stage_load<BKC>(rb, B, ldb, N, K, n0, 0, tid);
+  const int nk = (k_end - k_begin + GBK - 1) / GBK;
+  stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin, tid);
+  stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin, tid);
   stage_store<AK>(ra, smem, tid);
   stage_store<BKC>(rb, smem + TILE_BYTES, tid);
   __syncthreads();
@@ -158,8 +164,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      stage_load<AK>(ra, A, lda, M, K, m0, (kt + 1) * GBK, tid);
-      stage_load<BKC>(rb, B, ldb, N, K, n0, (kt + 1) * GBK, tid);
+      stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin + (kt + 1) * GBK, tid);
+      stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin + (kt + 1) * GBK, tid);
     }
     const char* a_s = smem + cur * 2 * TILE_BYTES;
     const char* b_s = a_s + TILE_BYTES;
@@ -183,6 +189,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   }
 
   const int g = lane >> 4, c16 = lane & 15;
+  if (ksplit > 1) {
+    // raw fp32 partial slab [split][M][N]; the reduce kernel applies the epilogue
+    float* slab = slabs + (long)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int row = m0 + wm * 64 + i * 16 + 4 * g + r, col = n0 + wn * 64 + j * 16 + c16;
+          if (row < M && col < N) slab[(long)row * N + col] = acc[i][j][r];
+        }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -191,6 +211,28 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
       for (int r = 0; r < 4; ++r)
         epi_apply<bf16>(e, M, N, m0 + wm * 64 + i * 16 + 4 * g + r, n0 + wn * 64 + j * 16 + c16,
                         acc[i][j][r]);
+}
+
+// Cf[m, n] (+)= alpha * sum_s slab[s][m][n]   (fixed order: deterministic)
+__global__ void splitk_reduce_kernel(int M, int N, int ksplit, const float* __restrict__ slabs,
+                                     float alpha, float* __restrict__ Cf, long ldcf,
+                                     int accumulate) {
+  long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  long MN = (long)M * N;
+  if (idx >= MN) return;
+  float4 a = *reinterpret_cast<const float4*>(slabs + idx);
+  for (int s = 1; s < ksplit; ++s) {
+    float4 b = *reinterpret_cast<const float4*>(slabs + (long)s * MN + idx);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  float v[4] = {a.x * alpha, a.y * alpha, a.z * alpha, a.w * alpha};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    long e = idx + t;
+    int row = e / N, col = e % N;
+    float* p = Cf + (long)row * ldcf + col;
+    *p = accumulate ? *p + v[t] : v[t];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -247,12 +289,40 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Split-K (deterministic slabs) for a pure Cf (+)= A.B^T epilogue with few
+// output tiles and a long K, i.e. the weight gradients (K = tokens): without
+// it a [512 x 1536] wgrad occupies 48 of 256 CUs.
+static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
+  bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
+  if (!cf_only) return 1;
+  long tiles = (long)((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+  if (tiles >= 512 || K < 1024 || ((long)M * N) % 4 != 0) return 1;
+  long s = (1024 + tiles - 1) / tiles;
+  s = std::min<long>(s, K / 512);
+  s = std::min<long>(s, (long)(ws_bytes / ((size_t)M * N * sizeof(float))));
+  s = std::max<long>(1, std::min<long>(s, 64));
+  return (int)s;
+}
+
 template <bool AK, bool BKC>
 static void launch_bf16(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                        const GemmEpi& e, hipStream_t s) {
-  int nwg = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
-  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC>), dim3(nwg), dim3(256), 4 * TILE_BYTES, s, M, N,
-                     K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+                        const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s) {
+  int tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+  int split = choose_split(M, N, K, e, ws ? ws_bytes : 0);
+  int kchunk = K;
+  if (split > 1) {
+    kchunk = ((K + split - 1) / split + GBK - 1) / GBK * GBK;
+    split = (K + kchunk - 1) / kchunk;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC>), dim3(tiles * split), dim3(256), 4 * TILE_BYTES,
+                     s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
+                     (float*)ws);
+  if (split > 1) {
+    long n4 = ((long)M * N) / 4;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,
+                       (const float*)ws, e.alpha, e.Cf, e.ldcf, e.accumulate);
+  }
 }
 template <bool AK, bool BKC>
 static void launch_f32(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
@@ -268,7 +338,8 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
                          const void* A, long lda, const void* B, long ldb, const float* bias,
                          float alpha, int relu, const void* residual, long ldr, const void* gate,
                          long ldg, float gate_scale, float drop_p, uint32_t drop_seed, void* C,
-                         long ldc, float* Cf, long ldcf, int accumulate, smer_stream_t stream) {
+                         long ldc, float* Cf, long ldcf, int accumulate, void* workspace,
+                         size_t ws_bytes, smer_stream_t stream) {
   SMER_REQUIRE(M >= 0 && N >= 0 && K >= 0, "smer_gemm: negative size");
   SMER_REQUIRE(A && B, "smer_gemm: null operand");
   SMER_REQUIRE(C || Cf, "smer_gemm: no output");
@@ -289,11 +360,12 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
                  "smer_gemm(bf16): column-image A needs lda >= round_up(M, 8)");
     SMER_REQUIRE(b_kcontig || ldb >= (long)((N + 7) / 8) * 8,
                  "smer_gemm(bf16): column-image B needs ldb >= round_up(N, 8)");
+    SMER_REQUIRE(!workspace || aligned16(workspace), "smer_gemm: workspace alignment");
     if (K == 0) return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm: K == 0");
-    if (a_kcontig && b_kcontig) launch_bf16<true, true>(M, N, K, A, lda, B, ldb, e, s);
-    else if (a_kcontig) launch_bf16<true, false>(M, N, K, A, lda, B, ldb, e, s);
-    else if (b_kcontig) launch_bf16<false, true>(M, N, K, A, lda, B, ldb, e, s);
-    else launch_bf16<false, false>(M, N, K, A, lda, B, ldb, e, s);
+    if (a_kcontig && b_kcontig) launch_bf16<true, true>(M, N, K, A, lda, B, ldb, e, workspace, ws_bytes, s);
+    else if (a_kcontig) launch_bf16<true, false>(M, N, K, A, lda, B, ldb, e, workspace, ws_bytes, s);
+    else if (b_kcontig) launch_bf16<false, true>(M, N, K, A, lda, B, ldb, e, workspace, ws_bytes, s);
+    else launch_bf16<false, false>(M, N, K, A, lda, B, ldb, e, workspace, ws_bytes, s);
   } else if (dtype == SMER_F32) {
     if (a_kcontig && b_kcontig) launch_f32<true, true>(M, N, K, A, lda, B, ldb, e, s);
     else if (a_kcontig) launch_f32<true, false>(M, N, K, A, lda, B, ldb, e, s);

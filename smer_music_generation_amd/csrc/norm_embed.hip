@@ -171,16 +171,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
   }
 }
 
-// out[col] (+)= sum_b part[b*stride + off + col]
-__global__ void col_reduce_kernel(int nblk, int N, const float* __restrict__ part, long stride,
-                                  long off, float* __restrict__ out, int accumulate, float scale) {
-  int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
-  float a = 0.f;
-  for (int b = 0; b < nblk; ++b) a += part[(long)b * stride + off + col];
-  a *= scale;
-  out[col] = accumulate ? out[col] + a : a;
-}
 
 // ---------------------------------------------------------------------------
 // embedding + sinusoidal PE
@@ -324,10 +314,10 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
   if (dgamma)
-    hipLaunchKernelGGL(col_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N, part,
+    hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N, part,
                        (long)2 * N, 0L, dgamma, accumulate, 1.f);
   if (dbeta)
-    hipLaunchKernelGGL(col_reduce_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N, part,
+    hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N, part,
                        (long)2 * N, (long)N, dbeta, accumulate, 1.f);
   SMER_CHECK_LAUNCH("smer_layernorm_bwd");
   return SMER_OK;

@@ -96,25 +96,68 @@ __global__ void cast_kernel(long n, const S* __restrict__ s, D* __restrict__ d) 
   for (; i < n; i += stride) d[i] = from_f32<D>(to_f32(s[i]));
 }
 
-constexpr int CS_ROWS = 128;
-template <typename T>
-__global__ void colsum_part_kernel(int M, int N, const T* __restrict__ x, long ldx,
-                                   float* __restrict__ part) {
-  int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
-  int r0 = blockIdx.y * CS_ROWS;
-  int r1 = min(M, r0 + CS_ROWS);
-  float a = 0.f;
-  for (int r = r0; r < r1; ++r) a += to_f32(x[(long)r * ldx + col]);
-  part[(long)blockIdx.y * N + col] = a;
+// Stage 1: workgroup = 512 columns (64 lanes x 8 via 16-B loads) x CS_ROWS
+// rows (4 row groups, 4 independent loads in flight each); fixed-order
+// combine of the 4 groups -> part[rowblock][N].
+constexpr int CS_ROWS = 256;
+template <typename T, bool VEC>
+__global__ __launch_bounds__(256) void colsum_part_kernel(int M, int N, const T* __restrict__ x,
+                                                          long ldx, float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 512 + cg * 8;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(M, r0 + CS_ROWS);
+  const int valid = VEC ? min(8, N - c0) : min(7, N - c0);  // <8 selects scalar loads
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (valid > 0) {
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      float v0[8], v1[8], v2[8], v3[8];
+      load8<T>(x + (long)r * ldx + c0, valid, v0);
+      load8<T>(x + (long)(r + 4) * ldx + c0, valid, v1);
+      load8<T>(x + (long)(r + 8) * ldx + c0, valid, v2);
+      load8<T>(x + (long)(r + 12) * ldx + c0, valid, v3);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += (v0[i] + v1[i]) + (v2[i] + v3[i]);
+    }
+    for (; r < r1; r += 4) {
+      float v0[8];
+      load8<T>(x + (long)r * ldx + c0, valid, v0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v0[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rg][cg * 8 + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    int col = blockIdx.x * 512 + c;
+    if (col < N) part[(long)blockIdx.y * N + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  }
 }
-__global__ void colsum_final_kernel(int nblk, int N, const float* __restrict__ part,
-                                    float* __restrict__ out, int accumulate) {
-  int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
-  float a = 0.f;
-  for (int b = 0; b < nblk; ++b) a += part[(long)b * N + col];
-  out[col] = accumulate ? out[col] + a : a;
+
+__global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const float* __restrict__ part,
+                                                       long stride, long off, float* __restrict__ out,
+                                                       int accumulate, float scale) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  float a0 = 0.f, a1 = 0.f;
+  if (col < N) {
+    int b = g;
+    for (; b + 4 < nblk; b += 8) {
+      a0 += part[(long)b * stride + off + col];
+      a1 += part[(long)(b + 4) * stride + off + col];
+    }
+    for (; b < nblk; b += 4) a0 += part[(long)b * stride + off + col];
+  }
+  red[g][cl] = a0 + a1;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    float a = ((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl])) * scale;
+    out[col] = accumulate ? out[col] + a : a;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -227,19 +270,21 @@ extern "C" int smer_colsum(int dtype, int M, int N, const void* x, long ldx, flo
   if (N == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   int nblk = (M + CS_ROWS - 1) / CS_ROWS;
-  dim3 grid((N + 255) / 256, nblk > 0 ? nblk : 1);
+  dim3 grid((N + 511) / 512, nblk > 0 ? nblk : 1);
+  bool vec = ((uintptr_t)x & 15) == 0 && ldx % 8 == 0;
   if (M > 0) {
-    if (dtype == SMER_BF16)
-      hipLaunchKernelGGL(colsum_part_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)x,
-                         ldx, (float*)workspace);
-    else if (dtype == SMER_F32)
-      hipLaunchKernelGGL(colsum_part_kernel<float>, grid, dim3(256), 0, s, M, N,
-                         (const float*)x, ldx, (float*)workspace);
-    else
+    if (dtype == SMER_BF16) {
+      if (vec) hipLaunchKernelGGL((colsum_part_kernel<bf16, true>), grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, (float*)workspace);
+      else hipLaunchKernelGGL((colsum_part_kernel<bf16, false>), grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, (float*)workspace);
+    } else if (dtype == SMER_F32) {
+      if (vec) hipLaunchKernelGGL((colsum_part_kernel<float, true>), grid, dim3(256), 0, s, M, N, (const float*)x, ldx, (float*)workspace);
+      else hipLaunchKernelGGL((colsum_part_kernel<float, false>), grid, dim3(256), 0, s, M, N, (const float*)x, ldx, (float*)workspace);
+    } else {
       return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_colsum: dtype");
+    }
   }
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, nblk, N,
-                     (const float*)workspace, out, accumulate);
+  hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N,
+                     (const float*)workspace, (long)N, 0L, out, accumulate, 1.f);
   SMER_CHECK_LAUNCH("smer_colsum");
   return SMER_OK;
 }

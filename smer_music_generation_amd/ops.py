@@ -76,14 +76,31 @@ def gemm(A, B, *, M, N, K, a_kcontig=True, b_kcontig=True, out=None, out_f32=Non
         timer.records.append((ev0, ev1, 2.0 * M * N * K))
 
 
+_SPLITK_WS = {}
+SPLITK_WS_BYTES = 64 << 20
+
+
+def splitk_workspace(device):
+    """Persistent per-device split-K slab buffer (stream-ordered reuse)."""
+    ws = _SPLITK_WS.get(device)
+    if ws is None:
+        ws = torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+        _SPLITK_WS[device] = ws
+    return ws
+
+
 def _gemm_call(dt, A, B, M, N, K, a_kcontig, b_kcontig, out, out_f32, accumulate, bias, alpha,
                relu, residual, gate, gate_scale, drop_p, seed):
+    ws = None
+    if out_f32 is not None and out is None and bias is None and residual is None and gate is None:
+        ws = splitk_workspace(A.device)
     call("smer_gemm", dt, int(a_kcontig), int(b_kcontig), M, N, K, _p(A), _ld(A), _p(B), _ld(B),
          _p(bias), float(alpha), int(relu), _p(residual),
          _ld(residual) if residual is not None else 0, _p(gate),
          _ld(gate) if gate is not None else 0, float(gate_scale), float(drop_p),
          int(seed) & 0xFFFFFFFF, _p(out), _ld(out) if out is not None else 0, _p(out_f32),
-         _ld(out_f32) if out_f32 is not None else 0, int(accumulate), _stream())
+         _ld(out_f32) if out_f32 is not None else 0, int(accumulate), _p(ws),
+         ws.numel() if ws is not None else 0, _stream())
 
 
 def linear(x, w, bias=None, *, out=None, out_f32=None, accumulate=False, relu=False,

@@ -61,6 +61,26 @@ def test_gemm_layouts(dtype, ak, bk, M, N, K):
     assert rel_err(Cf, ref) < (2e-3 if dtype == torch.bfloat16 else 1e-5)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 384, 8192), (309, 512, 4096), (1536, 512, 16384)])
+def test_gemm_splitk_wgrad(M, N, K):
+    """Weight-gradient shape (both operands column images, long K): the
+    deterministic split-K slab path must equal the unsplit result."""
+    O = ops()
+    dy = torch.randn(K, (M + 7) // 8 * 8, device=dev).to(torch.bfloat16)
+    x = torch.randn(K, N, device=dev).to(torch.bfloat16)
+    ref = dy[:, :M].float().t() @ x.float()
+    base = torch.randn(M, N, device=dev)
+    out = base.clone()
+    O.gemm(dy, x, M=M, N=N, K=K, a_kcontig=False, b_kcontig=False, out_f32=out, accumulate=True,
+           dtype=torch.bfloat16)
+    out2 = base.clone()
+    O.gemm(dy, x, M=M, N=N, K=K, a_kcontig=False, b_kcontig=False, out_f32=out2, accumulate=True,
+           dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    assert rel_err(out - base, ref) < 2e-3
+    assert torch.equal(out, out2)  # deterministic
+
+
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128
