@@ -59,16 +59,17 @@ static inline uint32_t smer_drop_threshold(float p) {
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
-// out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order.
-// Workgroup = 64 columns x 4 partial-row groups; deterministic.
-__global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const float* __restrict__ part,
-                                                       long stride, long off, float* __restrict__ out,
-                                                       int accumulate, float scale);
+// out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order
+// (deterministic; two levels when nblk > 64, `scratch` of
+// smer_col_reduce_scratch(nblk, N) bytes).  Defined in train_ops.hip.
+size_t smer_col_reduce_scratch(int nblk, int N);
+void smer_col_reduce_launch(int nblk, int N, const float* part, long stride, long off, float* out,
+                            int accumulate, float scale, float* scratch, hipStream_t s);
 
 // Load 8 consecutive elements as floats (16-B vector when aligned & in range).
-template <typename T>
+template <typename T, bool VEC = true>
 __device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
-  if (valid >= 8) {
+  if (VEC && valid >= 8) {
     if constexpr (sizeof(T) == 2) {
       bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
 #pragma unroll

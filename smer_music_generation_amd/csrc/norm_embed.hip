@@ -285,7 +285,7 @@ extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long l
 
 extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
   size_t nblk = (size_t)(M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-  return nblk * 2 * N * sizeof(float);
+  return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, N);
 }
 
 extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
@@ -314,11 +314,11 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
   if (dgamma)
-    hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N, part,
-                       (long)2 * N, 0L, dgamma, accumulate, 1.f);
+    smer_col_reduce_launch(nblk, N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
+                           part + (size_t)nblk * 2 * N, s);
   if (dbeta)
-    hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N, part,
-                       (long)2 * N, (long)N, dbeta, accumulate, 1.f);
+    smer_col_reduce_launch(nblk, N, part, (long)2 * N, (long)N, dbeta, accumulate, 1.f,
+                           part + (size_t)nblk * 2 * N, s);
   SMER_CHECK_LAUNCH("smer_layernorm_bwd");
   return SMER_OK;
 }

@@ -99,7 +99,7 @@ __global__ void cast_kernel(long n, const S* __restrict__ s, D* __restrict__ d) 
 // Stage 1: workgroup = 512 columns (64 lanes x 8 via 16-B loads) x CS_ROWS
 // rows (4 row groups, 4 independent loads in flight each); fixed-order
 // combine of the 4 groups -> part[rowblock][N].
-constexpr int CS_ROWS = 256;
+constexpr int CS_ROWS = 64;
 template <typename T, bool VEC>
 __global__ __launch_bounds__(256) void colsum_part_kernel(int M, int N, const T* __restrict__ x,
                                                           long ldx, float* __restrict__ part) {
@@ -108,22 +108,22 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(int M, int N, const T*
   const int c0 = blockIdx.x * 512 + cg * 8;
   const int r0 = blockIdx.y * CS_ROWS;
   const int r1 = min(M, r0 + CS_ROWS);
-  const int valid = VEC ? min(8, N - c0) : min(7, N - c0);  // <8 selects scalar loads
+  const int valid = min(8, N - c0);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (valid > 0) {
     int r = r0 + rg;
     for (; r + 12 < r1; r += 16) {
       float v0[8], v1[8], v2[8], v3[8];
-      load8<T>(x + (long)r * ldx + c0, valid, v0);
-      load8<T>(x + (long)(r + 4) * ldx + c0, valid, v1);
-      load8<T>(x + (long)(r + 8) * ldx + c0, valid, v2);
-      load8<T>(x + (long)(r + 12) * ldx + c0, valid, v3);
+      load8<T, VEC>(x + (long)r * ldx + c0, valid, v0);
+      load8<T, VEC>(x + (long)(r + 4) * ldx + c0, valid, v1);
+      load8<T, VEC>(x + (long)(r + 8) * ldx + c0, valid, v2);
+      load8<T, VEC>(x + (long)(r + 12) * ldx + c0, valid, v3);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += (v0[i] + v1[i]) + (v2[i] + v3[i]);
     }
     for (; r < r1; r += 4) {
       float v0[8];
-      load8<T>(x + (long)r * ldx + c0, valid, v0);
+      load8<T, VEC>(x + (long)r * ldx + c0, valid, v0);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += v0[i];
     }
@@ -137,26 +137,53 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(int M, int N, const T*
   }
 }
 
+// Workgroup (x = 64-column tile, y = chunk of `chunk` partial rows) writes
+// out[y * ostride + col]; rows summed in a fixed order (deterministic).
 __global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const float* __restrict__ part,
                                                        long stride, long off, float* __restrict__ out,
-                                                       int accumulate, float scale) {
+                                                       long ostride, int chunk, int accumulate,
+                                                       float scale) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
-  float a0 = 0.f, a1 = 0.f;
+  const int b0 = blockIdx.y * chunk, b1 = min(nblk, b0 + chunk);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (col < N) {
-    int b = g;
-    for (; b + 4 < nblk; b += 8) {
-      a0 += part[(long)b * stride + off + col];
-      a1 += part[(long)(b + 4) * stride + off + col];
+    const float* p = part + off + col;
+    int b = b0 + g;
+    for (; b + 12 < b1; b += 16) {
+      a0 += p[(long)b * stride];
+      a1 += p[(long)(b + 4) * stride];
+      a2 += p[(long)(b + 8) * stride];
+      a3 += p[(long)(b + 12) * stride];
     }
-    for (; b < nblk; b += 4) a0 += part[(long)b * stride + off + col];
+    for (; b < b1; b += 4) a0 += p[(long)b * stride];
   }
-  red[g][cl] = a0 + a1;
+  red[g][cl] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (g == 0 && col < N) {
     float a = ((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl])) * scale;
-    out[col] = accumulate ? out[col] + a : a;
+    float* o = out + (long)blockIdx.y * ostride + col;
+    *o = accumulate ? *o + a : a;
+  }
+}
+
+size_t smer_col_reduce_scratch(int nblk, int N) {
+  return nblk > 64 ? (size_t)((nblk + 63) / 64) * N * sizeof(float) : 0;
+}
+
+void smer_col_reduce_launch(int nblk, int N, const float* part, long stride, long off, float* out,
+                            int accumulate, float scale, float* scratch, hipStream_t s) {
+  dim3 gx((N + 63) / 64);
+  if (nblk > 64) {
+    int g = (nblk + 63) / 64;
+    hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, g), dim3(256), 0, s, nblk, N, part, stride,
+                       off, scratch, (long)N, 64, 0, 1.f);
+    hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, 1), dim3(256), 0, s, g, N,
+                       (const float*)scratch, (long)N, 0L, out, 0L, g, accumulate, scale);
+  } else {
+    hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, 1), dim3(256), 0, s, nblk, N, part, stride,
+                       off, out, 0L, nblk, accumulate, scale);
   }
 }
 
@@ -259,7 +286,8 @@ extern "C" int smer_cast2d(int src_dtype, int dst_dtype, int rows, int cols, con
 }
 
 extern "C" size_t smer_colsum_workspace(int M, int N) {
-  return (size_t)((M + CS_ROWS - 1) / CS_ROWS) * N * sizeof(float);
+  size_t nblk = (size_t)(M + CS_ROWS - 1) / CS_ROWS;
+  return nblk * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, N);
 }
 
 extern "C" int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out,
@@ -283,8 +311,8 @@ extern "C" int smer_colsum(int dtype, int M, int N, const void* x, long ldx, flo
       return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_colsum: dtype");
     }
   }
-  hipLaunchKernelGGL(smer_col_reduce, dim3((N + 63) / 64), dim3(256), 0, s, nblk, N,
-                     (const float*)workspace, (long)N, 0L, out, accumulate, 1.f);
+  smer_col_reduce_launch(nblk, N, (const float*)workspace, (long)N, 0L, out, accumulate, 1.f,
+                         (float*)workspace + (size_t)nblk * N, s);
   SMER_CHECK_LAUNCH("smer_colsum");
   return SMER_OK;
 }

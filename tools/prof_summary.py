@@ -1,0 +1,15 @@
+"""Summarise a rocprofv3 --stats kernel_stats.csv (per-step when --steps given)."""
+import csv
+import sys
+
+path = sys.argv[1]
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+rows = list(csv.DictReader(open(path)))
+tot = sum(float(r['TotalDurationNs']) for r in rows)
+print("%-70s %6s %9s %9s %6s" % ("kernel", "calls", "avg_us", "ms/step", "%"))
+for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:int(sys.argv[3]) if len(sys.argv) > 3 else 25]:
+    name = r['Name'].replace('void ', '')[:70]
+    print("%-70s %6s %9.1f %9.3f %6.2f" % (name, r['Calls'], float(r['AverageNs']) / 1e3,
+                                          float(r['TotalDurationNs']) / 1e6 / steps,
+                                          100 * float(r['TotalDurationNs']) / tot))
+print("total kernel time per step: %.3f ms" % (tot / 1e6 / steps))
