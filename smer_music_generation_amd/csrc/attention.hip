@@ -148,16 +148,30 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
     }
     float x[4][4];
     float tmax = -INFINITY;
+    // padded / out-of-range keys of this tile as one wave-uniform bitmask
+    const int kl = t * KVB + lane;
+    const unsigned long long kbad = __ballot(kl >= Lk || (kp && kp[min(kl, Lk - 1)]));
+    const int q0w = (int)blockIdx.x * 64 + wave * 16;
+    if (kbad != 0ull || (causal && t * KVB + KVB - 1 > q0w)) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int key = t * KVB + mt * 16 + 4 * g + r;
-        bool ok = key < Lk && (!kp || !kp[key]) && (!causal || key <= qi);
-        float xv = ok ? st[mt][r] * c : -INFINITY;
-        x[mt][r] = xv;
-        tmax = fmaxf(tmax, xv);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int kk = mt * 16 + 4 * g + r;
+          const bool ok = !((kbad >> kk) & 1ull) && (!causal || t * KVB + kk <= qi);
+          const float xv = ok ? st[mt][r] * c : -INFINITY;
+          x[mt][r] = xv;
+          tmax = fmaxf(tmax, xv);
+        }
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[mt][r] = st[mt][r] * c;
+          tmax = fmaxf(tmax, x[mt][r]);
+        }
+    }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
@@ -385,6 +399,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
     float ds[4][4];
+    const int kl = t * KVB + lane;
+    const unsigned long long kbad = __ballot(kl >= Lk || (kp && kp[min(kl, Lk - 1)]));
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
@@ -395,8 +411,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int key = t * KVB + mt * 16 + 4 * g + r;
-        bool ok = qvalid && key < Lk && (!kp || !kp[key]) && (!causal || key <= qi);
+        const int kk = mt * 16 + 4 * g + r;
+        const int key = t * KVB + kk;
+        const bool ok = qvalid && !((kbad >> kk) & 1ull) && (!causal || key <= qi);
         float pv = ok ? exp2f(sacc[r] * c - lse2) : 0.f;
         float dpv = dpacc[r];
         if (drop_thr)

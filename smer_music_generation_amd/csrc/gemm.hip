@@ -30,6 +30,7 @@ struct GemmEpi {
   float* Cf;
   long ldcf;
   int accumulate;
+  int vec;  // every operand 16-B aligned with row strides % 8 == 0
 };
 
 template <typename T>
@@ -49,6 +50,63 @@ __device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int ro
   if (e.Cf) {
     float* p = e.Cf + (long)row * e.ldcf + col;
     *p = e.accumulate ? *p + v : v;
+  }
+}
+
+// Eight consecutive columns of one row (bf16 activations).  Vector path when
+// the host verified 16-B alignment of every operand (e.vec) and the chunk is
+// full; otherwise per element.
+__device__ __forceinline__ void epi_apply8(const GemmEpi& e, int M, int N, int row, int col,
+                                           float (&v)[8]) {
+  const int valid = min(8, N - col);
+  if (!e.vec || valid < 8) {
+    for (int k = 0; k < valid; ++k) epi_apply<bf16>(e, M, N, row, col + k, v[k]);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+  if (e.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (e.relu) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (e.drop_thr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      v[k] = smer_keep(e.seed, e.drop_thr, (uint32_t)row, (uint32_t)(col + k)) ? v[k] * e.drop_scale : 0.f;
+  }
+  if (e.residual) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)row * e.ldr + col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += (float)r[k];
+  }
+  if (e.gate) {
+    const bf16x8 gt = *reinterpret_cast<const bf16x8*>((const bf16*)e.gate + (long)row * e.ldg + col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (float)gt[k] > 0.f ? v[k] * e.gate_scale : 0.f;
+  }
+  if (e.C) {
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+    *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)row * e.ldc + col) = o;
+  }
+  if (e.Cf) {
+    float* p = e.Cf + (long)row * e.ldcf + col;
+    float4 o0 = make_float4(v[0], v[1], v[2], v[3]), o1 = make_float4(v[4], v[5], v[6], v[7]);
+    if (e.accumulate) {
+      const float4 a0 = *reinterpret_cast<const float4*>(p);
+      const float4 a1 = *reinterpret_cast<const float4*>(p + 4);
+      o0.x += a0.x; o0.y += a0.y; o0.z += a0.z; o0.w += a0.w;
+      o1.x += a1.x; o1.y += a1.y; o1.z += a1.z; o1.w += a1.w;
+    }
+    *reinterpret_cast<float4*>(p) = o0;
+    *reinterpret_cast<float4*>(p + 4) = o1;
   }
 }
 
@@ -188,29 +246,52 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
     __syncthreads();
   }
 
+  // Epilogue through LDS: each wave-half (wm) parks its 64x128 fp32 tile in
+  // LDS, then all 256 threads walk it row-contiguously, 8 columns each, so
+  // bias / residual / gate reads and C / Cf / slab writes are 16-B vectors
+  // and 16 consecutive lanes cover one 256-B (bf16) row segment.
   const int g = lane >> 4, c16 = lane & 15;
-  if (ksplit > 1) {
-    // raw fp32 partial slab [split][M][N]; the reduce kernel applies the epilogue
-    float* slab = slabs + (long)split * M * N;
+  constexpr int EP_LD = GBN + 4;
+  float* ep = reinterpret_cast<float*>(smem);
+  float* slab = ksplit > 1 ? slabs + (long)split * M * N : nullptr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int row = m0 + wm * 64 + i * 16 + 4 * g + r, col = n0 + wn * 64 + j * 16 + c16;
-          if (row < M && col < N) slab[(long)row * N + col] = acc[i][j][r];
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ep[(i * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int item = tid + 256 * c;
+      const int row = item >> 4, ch = item & 15;
+      const int grow = m0 + half * 64 + row, gcol = n0 + ch * 8;
+      if (grow < M && gcol < N) {
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+        const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        if (slab) {
+          const int valid = min(8, N - gcol);
+          float* dst = slab + (long)grow * N + gcol;
+          if (valid == 8 && (N & 3) == 0) {
+            *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+          } else {
+            for (int k = 0; k < valid; ++k) dst[k] = v[k];
+          }
+        } else {
+          epi_apply8(e, M, N, grow, gcol, v);
         }
-    return;
+      }
+    }
+    __syncthreads();
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        epi_apply<bf16>(e, M, N, m0 + wm * 64 + i * 16 + 4 * g + r, n0 + wn * 64 + j * 16 + c16,
-                        acc[i][j][r]);
 }
 
 // Cf[m, n] (+)= alpha * sum_s slab[s][m][n]   (fixed order: deterministic)
@@ -351,6 +432,8 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
   e.drop_thr = smer_drop_threshold(drop_p); e.seed = drop_seed;
   e.drop_scale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf; e.accumulate = accumulate;
+  auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
+  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(gate, ldg) && a16(C, ldc) && a16(Cf, ldcf);
   hipStream_t s = (hipStream_t)stream;
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(K % 8 == 0, "smer_gemm(bf16): K must be a multiple of 8");
