@@ -93,8 +93,10 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int qi = blockIdx.x * 64 + wave * 16 + c16;
+  int BX, BY;
+  xcd_block2d(BX, BY);
+  const int bh = BY, b = bh / H, h = bh % H;
+  const int qi = BX * 64 + wave * 16 + c16;
   const bool qvalid = qi < Lq;
   const float c = scale * LOG2E_F;
 
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
 
   int n_tiles = (Lk + KVB - 1) / KVB;
   if (causal) {
-    int qmax = min(Lq, (int)blockIdx.x * 64 + 64);
+    int qmax = min(Lq, BX * 64 + 64);
     n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
   }
   float m_run = -INFINITY, l_run = 0.f;
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
     // padded / out-of-range keys of this tile as one wave-uniform bitmask
     const int kl = t * KVB + lane;
     const unsigned long long kbad = __ballot(kl >= Lk || (kp && kp[min(kl, Lk - 1)]));
-    const int q0w = (int)blockIdx.x * 64 + wave * 16;
+    const int q0w = BX * 64 + wave * 16;
     if (kbad != 0ull || (causal && t * KVB + KVB - 1 > q0w)) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -237,8 +239,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
   __shared__ float s_lse[2][KVB], s_del[2][KVB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int kj = blockIdx.x * 64 + wave * 16 + c16;
+  int BX, BY;
+  xcd_block2d(BX, BY);
+  const int bh = BY, b = bh / H, h = bh % H;
+  const int kj = BX * 64 + wave * 16 + c16;
   const bool kvalid = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
   const float c = scale * LOG2E_F;
 
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
   const float* db = delta + (long)bh * Lq;
 
   const int n_qt = (Lq + KVB - 1) / KVB;
-  const int t0 = causal ? min(n_qt, (int)(blockIdx.x * 64) / KVB) : 0;
+  const int t0 = causal ? min(n_qt, (BX * 64) / KVB) : 0;
   f32x4 adk[C::NDT], adv[C::NDT];
 #pragma unroll
   for (int i = 0; i < C::NDT; ++i) { adk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; adv[i] = adk[i]; }
@@ -353,8 +357,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
-  const int qi = blockIdx.x * 64 + wave * 16 + c16;
+  int BX, BY;
+  xcd_block2d(BX, BY);
+  const int bh = BY, b = bh / H, h = bh % H;
+  const int qi = BX * 64 + wave * 16 + c16;
   const bool qvalid = qi < Lq;
   const float c = scale * LOG2E_F;
   bf16x8 qf[C::NS], of[C::NS];
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
   const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
   int n_tiles = (Lk + KVB - 1) / KVB;
   if (causal) {
-    int qmax = min(Lq, (int)blockIdx.x * 64 + 64);
+    int qmax = min(Lq, BX * 64 + 64);
     n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
   }
   f32x4 adq[C::NDT];

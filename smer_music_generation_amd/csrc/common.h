@@ -84,6 +84,19 @@ __device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
   }
 }
 
+// XCD-aware 2-D block index: blocks b and b+8 share an XCD (round-robin
+// dispatch), so give each XCD a contiguous run of the row-major work list;
+// x-neighbours (e.g. the query blocks of one (batch, head)) then share an L2.
+// Bijective for any grid size.  Speed only, never correctness.
+__device__ __forceinline__ void xcd_block2d(int& bx, int& by) {
+  const int nx = gridDim.x, n = gridDim.x * gridDim.y;
+  const int b = blockIdx.y * nx + blockIdx.x;
+  const int xcd = b & 7, q = n >> 3, r = n & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  bx = lin % nx;
+  by = lin / nx;
+}
+
 __device__ __forceinline__ bf16x8 lds_read_b128(const char* base, uint32_t byte_off) {
   return *reinterpret_cast<const bf16x8*>(base + byte_off);
 }

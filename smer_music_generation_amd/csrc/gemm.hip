@@ -192,8 +192,11 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   const int braw = blockIdx.x;
   const int xcd = braw & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (braw >> 3);
-  const int split = lin % ksplit;
-  const int wgid = lin / ksplit;
+  // tile-major within a K slice: blocks that run together on one XCD share
+  // the slice's A and B panels in that XCD's L2
+  const int ntiles = nbm * nbn;
+  const int split = lin / ntiles;
+  const int wgid = lin % ntiles;
   constexpr int GM = 8;
   const int grp = wgid / (GM * nbn);
   const int first_m = grp * GM;
