@@ -131,6 +131,8 @@ def bench_infill(args, dev, rank):
     dt = time.perf_counter() - t0
     src_len = float(np.mean([len(r[0]) for r in reqs]))
     return {"tokens": st["tokens"], "steps": st["steps"], "seconds": dt,
+            "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s",
+                                                      "step_call_s")},
             "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len}
 
 
@@ -165,7 +167,7 @@ def cpu_baseline(args):
                       % (n, B, args.seq, args.tgt)}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -182,7 +184,11 @@ def main():
     ap.add_argument("--no-infill", dest="infill", action="store_false")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--no-roofline", dest="roofline", action="store_false")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -238,7 +244,7 @@ def main():
                                "requests_per_gpu": inf["requests"],
                                "mean_src_len": round(inf["mean_src_len"], 1),
                                "decode_steps": inf["steps"], "tokens": inf["tokens"],
-                               "parallelism": "replicas"},
+                               "phases_s": inf["phases_s"], "parallelism": "replicas"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

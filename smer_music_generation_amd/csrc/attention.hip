@@ -729,6 +729,119 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(int H, int D, const T*
   }
 }
 
+// Vectorised single-pass decode attention (online softmax).  One block per
+// (row, head), 4 waves.  LPK lanes own one key (each lane a 16-B slice of
+// D = LPK*VEC), so a wave walks 64/LPK keys per step with 16-B K and V
+// loads; UNR steps are issued together to keep loads in flight.  Each lane
+// group keeps a running (max, sum, acc[VEC]); groups are merged with
+// shuffles, waves through LDS.
+template <typename T>
+__device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)t[i];
+  } else {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+}
+template <typename T, int LPK, int UNR>
+__global__ __launch_bounds__(256) void attn_decode_vec_kernel(
+    const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
+    long row_stride, long req_stride, const int32_t* __restrict__ row_req,
+    const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int D = LPK * VEC;
+  constexpr int GPW = 64 / LPK;  // key groups per wave
+  constexpr int KPB = 4 * GPW;   // keys per block step
+  __shared__ float red_m[4][LPK], red_l[4][LPK], red_a[4][LPK][VEC];
+  const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int sub = lane % LPK, grp = wave * GPW + lane / LPK;
+  const int nk = row_nkeys[r];
+  const long base = (long)row_req[r] * req_stride + h * D + sub * VEC;
+  float qv[VEC];
+  load16b<T>(q + (long)r * ldq + h * D + sub * VEC, qv);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) qv[i] *= scale;
+  float m = -INFINITY, l = 0.f, acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
+    float kv[UNR][VEC], vv[UNR][VEC];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = j0 + u * KPB + grp;
+      const bool ok = j < nk;
+      const long off = base + (long)(ok ? j : 0) * row_stride;
+      load16b<T>(kc + off, kv[u]);
+      load16b<T>(vc + off, vv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = j0 + u * KPB + grp;
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) s = fmaf(qv[i], kv[u][i], s);
+#pragma unroll
+      for (int w = 1; w < LPK; w <<= 1) s += __shfl_xor(s, w, 64);
+      if (j < nk) {
+        const float mn = fmaxf(m, s);
+        const float c = __expf(m - mn), p = __expf(s - mn);
+        l = l * c + p;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], c, p * vv[u][i]);
+        m = mn;
+      }
+    }
+  }
+  // merge the groups of a wave (lanes with equal `sub`)
+#pragma unroll
+  for (int w = LPK; w < 64; w <<= 1) {
+    const float mo = __shfl_xor(m, w, 64), lo = __shfl_xor(l, w, 64);
+    const float mn = fmaxf(m, mo);
+    const float c0 = m == -INFINITY ? 0.f : __expf(m - mn);
+    const float c1 = mo == -INFINITY ? 0.f : __expf(mo - mn);
+    l = l * c0 + lo * c1;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = acc[i] * c0 + __shfl_xor(acc[i], w, 64) * c1;
+    m = mn;
+  }
+  if (lane < LPK) {
+    red_m[wave][lane] = m;
+    red_l[wave][lane] = l;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) red_a[wave][lane][i] = acc[i];
+  }
+  __syncthreads();
+  if (tid < LPK) {
+    float mm = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mm = fmaxf(mm, red_m[w][tid]);
+    float ll = 0.f, out[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) out[i] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float c = red_m[w][tid] == -INFINITY ? 0.f : __expf(red_m[w][tid] - mm);
+      ll += red_l[w][tid] * c;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) out[i] += red_a[w][tid][i] * c;
+    }
+    const float inv = ll > 0.f ? 1.f / ll : 0.f;
+    T* op = o + (long)r * ldo + h * D + tid * VEC;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 t;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) t[i] = (bf16)(out[i] * inv);
+      *reinterpret_cast<bf16x8*>(op) = t;
+    } else {
+      *reinterpret_cast<float4*>(op) = make_float4(out[0] * inv, out[1] * inv, out[2] * inv, out[3] * inv);
+    }
+  }
+}
+
 template <typename T>
 __global__ void kv_scatter_kernel(int n_rows, int width, const T* __restrict__ src, long lds,
                                   T* __restrict__ cache, long row_stride, long req_stride,
@@ -888,6 +1001,31 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
                                 smer_stream_t stream) {
   SMER_REQUIRE(D <= 256, "smer_attn_decode: head dim <= 256");
   if (n_rows == 0) return SMER_OK;
+  {
+    // vectorised path: 16-B aligned rows, LPK = D / (16 / elem) in {4, 8, 16}
+    const int es = dtype == SMER_BF16 ? 2 : 4, vec = 16 / es;
+    auto al = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+    const bool ok = (dtype == SMER_BF16 || dtype == SMER_F32) && D % vec == 0 && al(q) &&
+                    al(kcache) && al(vcache) && al(o) && ldq % vec == 0 && ldo % vec == 0 &&
+                    row_stride % vec == 0 && req_stride % vec == 0;
+    const int lpk = D / vec;
+    hipStream_t s = (hipStream_t)stream;
+    dim3 grid(n_rows, H);
+#define SMER_DEC_VEC(T, L)                                                                       \
+  hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 2>), grid, dim3(256), 0, s, (const T*)q, ldq, \
+                     (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,          \
+                     row_nkeys, (T*)o, ldo, scale)
+    if (ok && (lpk == 4 || lpk == 8 || lpk == 16)) {
+      if (dtype == SMER_BF16) {
+        if (lpk == 4) SMER_DEC_VEC(bf16, 4); else if (lpk == 8) SMER_DEC_VEC(bf16, 8); else SMER_DEC_VEC(bf16, 16);
+      } else {
+        if (lpk == 4) SMER_DEC_VEC(float, 4); else if (lpk == 8) SMER_DEC_VEC(float, 8); else SMER_DEC_VEC(float, 16);
+      }
+#undef SMER_DEC_VEC
+      SMER_CHECK_LAUNCH("smer_attn_decode");
+      return SMER_OK;
+    }
+  }
   // key capacity bounded by req_stride / row_stride rows
   long cap = req_stride / (row_stride > 0 ? row_stride : 1);
   SMER_REQUIRE(cap > 0 && cap * 4 <= 150 * 1024, "smer_attn_decode: cache capacity too large");

@@ -297,6 +297,81 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Skinny bf16 NT GEMM (M <= 256: decode steps, tiny batches).  The 128x128
+// tile kernel would run 4-16 workgroups there; this one gives each
+// workgroup a 64-row x 16-column output strip and splits K over its 8 waves.
+// MFMA fragments are loaded straight from global memory (both operands are
+// K-contiguous: every fragment is one 16-B load per lane), the 8 per-wave
+// partial tiles are summed through LDS in fixed order (deterministic), then
+// the shared epilogue runs on 8-column vectors.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int SK_BM = 64, SK_BN = 16, SK_WAVES = 8, SK_UNR = 2;
+}
+__global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int K,
+                                                               const bf16* __restrict__ A, long lda,
+                                                               const bf16* __restrict__ B, long ldb,
+                                                               GemmEpi e) {
+  __shared__ float red[SK_WAVES][SK_BM][SK_BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * SK_BN, m0 = blockIdx.y * SK_BM;
+  const int r16 = lane & 15, kq = (lane >> 4) * 8;
+  const int ncol = n0 + r16;
+  const bool colok = ncol < N;
+  const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
+  const bf16* ap[4];
+  bool rowok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + i * 16 + r16;
+    rowok[i] = row < M;
+    ap[i] = A + (long)(rowok[i] ? row : 0) * lda + kq;
+  }
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (K + 31) / 32;
+  for (int s0 = wave; s0 < nsteps; s0 += SK_WAVES * SK_UNR) {
+    bf16x8 a[SK_UNR][4], b[SK_UNR];
+#pragma unroll
+    for (int u = 0; u < SK_UNR; ++u) {
+      const int k = (s0 + u * SK_WAVES) * 32;
+      const bool kok = k + kq < K;  // K % 8 == 0: a lane's 8-chunk is all in or all out
+      b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[u][i] = (rowok[i] && kok) ? *reinterpret_cast<const bf16x8*>(ap[i] + k) : bf16x8{};
+    }
+#pragma unroll
+    for (int u = 0; u < SK_UNR; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
+  }
+  // D[row 4g+r][col c16] of each 16x16 tile
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][i * 16 + 4 * g + r][r16] = acc[i][r];
+  __syncthreads();
+  if (tid < SK_BM * 2) {
+    const int row = tid >> 1, ch = tid & 1;
+    const int grow = m0 + row, gcol = n0 + ch * 8;
+    if (grow < M && gcol < N) {
+      float v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < SK_WAVES; ++w) t += red[w][row][ch * 8 + c];
+        v[c] = t;
+      }
+      epi_apply8(e, M, N, grow, gcol, v);
+    }
+  }
+}
+
 // Cf[m, n] (+)= alpha * sum_s slab[s][m][n]   (fixed order: deterministic)
 __global__ void splitk_reduce_kernel(int M, int N, int ksplit, const float* __restrict__ slabs,
                                      float alpha, float* __restrict__ Cf, long ldcf,
@@ -392,6 +467,11 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
 template <bool AK, bool BKC>
 static void launch_bf16(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                         const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (AK && BKC && M <= 4 * SK_BM) {
+    hipLaunchKernelGGL(gemm_skinny_bf16_kernel, dim3((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM),
+                       dim3(64 * SK_WAVES), 0, s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+    return;
+  }
   int tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   int split = choose_split(M, N, K, e, ws ? ws_bytes : 0);
   int kchunk = K;

@@ -12,6 +12,14 @@ Here, per request:
 Mathematically identical to the full recompute (causal attention: earlier
 positions never see later tokens); fp32 mode reproduces the reference logits
 to ~1e-6 and its greedy token ids exactly.
+
+Fixed-shape step: every request owns TWO row slots per step (a feed is one
+token, or two right after a control span: the control token + the next
+m_0).  Unused slots are dummies that write their K/V into a reserved trash
+position (Tmax-1, never attended).  The step shape is therefore constant and
+is captured ONCE into a HIP graph (torch.cuda.CUDAGraph drives stream
+capture; every kernel is a libsmer_hip.so launch on the captured stream) and
+replayed per token: one H2D of the row table, one replay, one D2H.
 """
 from __future__ import annotations
 
@@ -24,7 +32,7 @@ from . import ops
 
 
 class DecodeSession:
-    def __init__(self, model, max_requests, max_src, max_tgt, precision=None):
+    def __init__(self, model, max_requests, max_src, max_tgt, precision=None, use_graph=True):
         if precision is not None:
             model.set_precision(precision)
         self.model = model
@@ -32,10 +40,11 @@ class DecodeSession:
         eng = self.eng
         self.dt = eng.act_dtype()
         dev = model.flat_parameters().device
-        if not dev.type == "cuda":
+        if dev.type != "cuda":
             raise RuntimeError("DecodeSession needs the model on a ROCm GPU")
         self.dev = dev
-        self.R, self.Smax, self.Tmax = int(max_requests), int(max_src), int(max_tgt)
+        self.R, self.Smax = int(max_requests), int(max_src)
+        self.Tmax = int(max_tgt) + 1  # + trash slot
         d = eng.d
         self.d = d
         if max(self.Smax, self.Tmax) > model.pos_enc.pe.shape[0]:
@@ -46,9 +55,21 @@ class DecodeSession:
                          for _ in range(eng.n_dec)]
         self.src_len = np.zeros(self.R, dtype=np.int64)
         self.W = eng.weights(self.dt)
+        # static step buffers: 2 slots per request
+        M = 2 * self.R
+        self.M = M
+        self.ids_t = torch.zeros(M, dtype=torch.int64, device=dev)
+        self.meta_t = torch.zeros(4, M, dtype=torch.int32, device=dev)
+        self.ids_h = torch.zeros(M, dtype=torch.int64).pin_memory()
+        self.meta_h = torch.zeros(4, M, dtype=torch.int32).pin_memory()
+        self.logits_h = torch.zeros(M, eng.V, dtype=torch.float32).pin_memory()
+        self.use_graph = use_graph
+        self.graph = None
+        self.logits_t = None
 
     def refresh_weights(self):
         self.W = self.eng.weights(self.dt)
+        self.graph = None
 
     # ------------------------------------------------------------------
     def prefill(self, slots, srcs):
@@ -84,49 +105,29 @@ class DecodeSession:
             y2 = ops.linear(h, L.l2_w, L.l2_b, residual=x1)
             x, _, _ = eng._ln(y2, L.n2, dt)
         mem, _, _ = eng._ln(x, W.enc_norm, dt)
-        # scatter the valid memory rows' cross K/V into the per-request caches
-        rows_b = np.concatenate([np.full(n, slots[b], dtype=np.int32) for b, n in enumerate(lens)])
-        rows_j = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
-        rows_src = np.concatenate([b * S + np.arange(n) for b, n in enumerate(lens)])
-        sel = torch.from_numpy(rows_src.astype(np.int64)).to(dev)
-        req_t = torch.from_numpy(rows_b).to(dev)
-        pos_t = torch.from_numpy(rows_j).to(dev)
-        mem_rows = mem if min(lens) == S else mem.index_select(0, sel)
+        # all B*S memory rows go to the caches (rows past a source's length
+        # land beyond its src_len and are never attended)
+        req = np.repeat(np.asarray(slots, dtype=np.int32), S)
+        pos = np.tile(np.arange(S, dtype=np.int32), B)
+        req_t = torch.from_numpy(req).to(dev)
+        pos_t = torch.from_numpy(pos).to(dev)
         for li, L in enumerate(W.dec):
-            kvc = ops.linear(mem_rows, L.ckv_w, L.ckv_b)
+            kvc = ops.linear(mem, L.ckv_w, L.ckv_b)
             ops.kv_scatter(kvc, self.cross_kv[li], req_t, pos_t, row_stride=2 * d,
                            req_stride=self.Smax * 2 * d)
         for b, s in enumerate(slots):
             self.src_len[s] = lens[b]
 
     # ------------------------------------------------------------------
-    def step(self, feeds):
-        """feeds: list of (slot, new_token_ids, first_position).  Returns fp32
-        logits [len(feeds), V] (numpy) of each feed's LAST new token."""
+    def _run(self):
+        """The fixed-shape decoder step on the static buffers."""
         eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
-        H, D = eng.H, eng.D
-        ids, pos, req, last = [], [], [], []
-        for slot, toks, p0 in feeds:
-            n = len(toks)
-            if p0 + n > self.Tmax:
-                raise ValueError("decoder prefix exceeds session max_tgt %d" % self.Tmax)
-            ids.extend(int(t) for t in toks)
-            pos.extend(range(p0, p0 + n))
-            req.extend([slot] * n)
-            last.append(len(ids) - 1)
-        M = len(ids)
-        meta = np.empty((4, M), dtype=np.int32)
-        meta[0] = pos
-        meta[1] = req
-        meta[2] = meta[0] + 1
-        meta[3] = self.src_len[meta[1]]
-        meta_t = torch.from_numpy(meta).to(dev, non_blocking=False)
-        ids_t = torch.tensor(ids, dtype=torch.int64, device=dev)
-        pos_t, req_t, nks_t, nkc_t = meta_t[0], meta_t[1], meta_t[2], meta_t[3]
+        H, D, M = eng.H, eng.D, self.M
+        pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
         pe = self.model.pos_enc.pe
         pe2 = pe.view(pe.shape[0], pe.shape[2])
         x = torch.empty(M, d, dtype=dt, device=dev)
-        ops.embed(ids_t, W.emb, pe2, x, positions=pos_t, scale=math.sqrt(d))
+        ops.embed(self.ids_t, W.emb, pe2, x, positions=pos_t, scale=math.sqrt(d))
         scale = 1.0 / math.sqrt(D)
         sstride = self.Tmax * 2 * d
         cstride = self.Smax * 2 * d
@@ -150,7 +151,59 @@ class DecodeSession:
             y3 = ops.linear(h, L.l2_w, L.l2_b, residual=x2)
             x, _, _ = eng._ln(y3, L.n3, dt)
         out, _, _ = eng._ln(x, W.dec_norm, dt)
-        logits = torch.empty(M, eng.V, device=dev)
+        logits = torch.empty(M, eng.V, device=dev) if self.logits_t is None else self.logits_t
         ops.gemm(out, W.fc_w, M=M, N=eng.V, K=d, out_f32=logits, bias=W.fc_b, dtype=dt)
-        lg = logits.cpu().numpy()
-        return lg[last]
+        self.logits_t = logits
+
+    def _ensure_graph(self):
+        if self.graph is not None or not self.use_graph:
+            return
+        # warm up eagerly once (allocator, library load), then capture
+        self._run()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._run()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = g
+
+    def step(self, feeds):
+        """feeds: list of (slot, new_token_ids (1 or 2), first_position).
+        Returns fp32 logits [len(feeds), V] (numpy) of each feed's LAST new
+        token.  Slots not fed this step are dummies."""
+        R, Tm = self.R, self.Tmax
+        ids = self.ids_h.numpy()
+        meta = self.meta_h.numpy()
+        ids[:] = 0
+        slots = np.arange(self.M, dtype=np.int32) // 2
+        meta[0] = Tm - 1           # dummy rows -> trash position
+        meta[1] = slots
+        meta[2] = 1                # dummy rows attend one key
+        meta[3] = 1
+        last = []
+        for slot, toks, p0 in feeds:
+            n = len(toks)
+            if n > 2:
+                raise ValueError("a feed carries at most 2 new tokens")
+            if p0 + n > Tm - 1:
+                raise ValueError("decoder prefix exceeds session max_tgt %d" % (Tm - 1))
+            r0 = 2 * slot + (2 - n)
+            for k in range(n):
+                ids[r0 + k] = int(toks[k])
+                meta[0, r0 + k] = p0 + k
+                meta[2, r0 + k] = p0 + k + 1
+                meta[3, r0 + k] = max(int(self.src_len[slot]), 1)
+            last.append(2 * slot + 1)
+        self.ids_t.copy_(self.ids_h, non_blocking=True)
+        self.meta_t.copy_(self.meta_h, non_blocking=True)
+        if self.use_graph:
+            self._ensure_graph()
+            self.graph.replay()
+        else:
+            self._run()
+        self.logits_h.copy_(self.logits_t, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        return self.logits_h.numpy()[last]

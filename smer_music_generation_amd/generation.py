@@ -19,6 +19,8 @@ the numpy RNG consumption are the reference's, so with the same
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
@@ -165,7 +167,7 @@ class _Span:
     def prefix(self):
         return self.tgt_inp + self.this_in
 
-    def _draw(self, logit, check, failmsg, **flags):
+    def _draw(self, logit, check, failmsg, flags):
         idx = sampling(logit, self.v, greedy=self.greedy, **flags)
         if check is None:
             return idx
@@ -179,36 +181,51 @@ class _Span:
                 break
         return idx
 
-    def advance(self, logit):
-        """Consume the logits of the current prefix's last position."""
+    def spec(self):
+        """(sampling flags, redraw check, failure message) of the current
+        grammar state (generation.py:549-630)."""
         v = self.v
         if self.in_sep:
-            idx = self._draw(logit, lambda i: i in v.rest_indices or i == v.eos_index or
-                             i == v.duration_only_indices[0], "in sep failed", no_rest=True,
-                             no_sep=True, no_eos=True, no_whole_duration=True, no_control=True)
-        elif self.in_continue:
-            idx = self._draw(logit, lambda i: i not in v.pitch_indices, 'in continue failed',
-                             no_rest=True, no_sep=True, no_duration=True, no_continue=True,
-                             no_eos=True, no_control=True)
-        elif self.in_pitch:
-            idx = self._draw(logit, lambda i: i not in v.duration_only_indices and
-                             i not in v.pitch_indices, 'in pitch failed', no_rest=True,
-                             no_sep=True, no_continue=True, no_whole_duration=self.no_whole,
-                             no_eos=True, no_control=True)
-        elif self.in_rest:
-            idx = self._draw(logit, lambda i: i not in v.duration_only_indices, 'in rest failed',
-                             no_pitch=True, no_rest=True, no_sep=True, no_continue=True,
-                             no_whole_duration=self.no_whole, no_eos=True, no_control=True)
-        elif len(self.this_in) == 1:
+            return (dict(no_rest=True, no_sep=True, no_eos=True, no_whole_duration=True,
+                         no_control=True),
+                    lambda i: i in v.rest_indices or i == v.eos_index or
+                    i == v.duration_only_indices[0], "in sep failed")
+        if self.in_continue:
+            return (dict(no_rest=True, no_sep=True, no_duration=True, no_continue=True,
+                         no_eos=True, no_control=True),
+                    lambda i: i not in v.pitch_indices, 'in continue failed')
+        if self.in_pitch:
+            return (dict(no_rest=True, no_sep=True, no_continue=True,
+                         no_whole_duration=self.no_whole, no_eos=True, no_control=True),
+                    lambda i: i not in v.duration_only_indices and i not in v.pitch_indices,
+                    'in pitch failed')
+        if self.in_rest:
+            return (dict(no_pitch=True, no_rest=True, no_sep=True, no_continue=True,
+                         no_whole_duration=self.no_whole, no_eos=True, no_control=True),
+                    lambda i: i not in v.duration_only_indices, 'in rest failed')
+        if len(self.this_in) == 1:
             tc = self.mask_target[self.mask_idx]
             if tc != 'r':
                 flag = {'d': 'is_density', 'o': 'is_occupation', 'p': 'is_polyphony'}.get(tc, 'is_tensile')
-                idx = self._draw(logit, None, '', **{flag: True})
-            else:
-                idx = self._draw(logit, lambda i: i in v.duration_only_indices, 'start failed',
-                                 no_duration=True, no_control=True)
-        else:
-            idx = self._draw(logit, None, '', no_whole_duration=self.no_whole, no_control=True)
+                return {flag: True}, None, ''
+            return (dict(no_duration=True, no_control=True),
+                    lambda i: i in v.duration_only_indices, 'start failed')
+        return dict(no_whole_duration=self.no_whole, no_control=True), None, ''
+
+    def advance(self, logit):
+        """Consume the logits of the current prefix's last position."""
+        flags, check, failmsg = self.spec()
+        return self.commit(self._draw(logit, check, failmsg, flags))
+
+    def commit_greedy(self, idx, check, failmsg):
+        """Greedy draw already taken (argmax over the masked logits): the
+        reference's redraw loop would re-draw the same id 11 times."""
+        if check is not None and check(int(idx)) and self.logger is not None:
+            self.logger.info(failmsg)
+        return self.commit(idx)
+
+    def commit(self, idx):
+        v = self.v
         idx = int(idx)
         ev = v.index2char(idx)
         if idx == v.continue_index:
@@ -294,6 +311,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     requests: list of (events, tracks_to_generate, bars_to_generate).
     Returns a list of (restored, mask_track_names, mask_bar_names) (None
     where nothing was masked), and optionally {'tokens', 'steps'}."""
+    t0 = time.perf_counter()
     preps = [_prepare(list(ev), vocab, tr, br) for ev, tr, br in requests]
     spans = [_Span(vocab, p[0], p[3], all_controls, p[4], greedy, logger) for p in preps]
     R = len(requests)
@@ -303,7 +321,11 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     tokens = steps = 0
     with torch.no_grad():
         sess = DecodeSession(model, R, Smax, Tmax, precision=precision)
+        t1 = time.perf_counter()
         sess.prefill(list(range(R)), [p[0] for p in preps])
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_dev = 0.0
         fed = [0] * R
         while True:
             live = [i for i in range(R) if not spans[i].done]
@@ -314,11 +336,21 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
                 pre = spans[i].prefix()
                 feeds.append((i, pre[fed[i]:], fed[i]))
                 fed[i] = len(pre)
+            ts = time.perf_counter()
             lg = sess.step(feeds)
-            for k, i in enumerate(live):
-                before = len(spans[i].tgt_inp) + len(spans[i].this_in)
-                spans[i].advance(lg[k])
-                tokens += 1
+            t_dev += time.perf_counter() - ts
+            if greedy:
+                # one masked argmax over all live rows (same ids as the
+                # per-row float64 softmax argmax: exp/normalise is monotone)
+                specs = [spans[i].spec() for i in live]
+                keep = np.stack([allowed_ids(vocab, **f) for f, _, _ in specs])
+                ids = np.argmax(np.where(keep, lg, np.float32(-100.0)), axis=1)
+                for k, i in enumerate(live):
+                    spans[i].commit_greedy(ids[k], specs[k][1], specs[k][2])
+            else:
+                for k, i in enumerate(live):
+                    spans[i].advance(lg[k])
+            tokens += len(live)
             steps += 1
     out = []
     for p, st in zip(preps, spans):
@@ -328,5 +360,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         src_token = [vocab.index2char(int(t)) for t in p[0]]
         out.append((restore_marked_input(src_token, st.total), p[1], p[2]))
     if return_stats:
-        return out, {"tokens": tokens, "steps": steps}
+        t3 = time.perf_counter()
+        return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,
+                     "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev}
     return out

@@ -93,9 +93,10 @@ def test_gemm_identity_asymmetric():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_gemm_epilogue(dtype):
+@pytest.mark.parametrize("M,N,K", [(192, 256, 128), (640, 264, 136), (40, 264, 136)])
+def test_gemm_epilogue(dtype, M, N, K):
+    """Skinny (M <= 256) and tiled kernels, incl. N and K tails."""
     O = ops()
-    M, N, K = 192, 256, 128
     A = torch.randn(M, K, device=dev).to(dtype)
     W = torch.randn(N, K, device=dev).to(dtype)
     bias = torch.randn(N, device=dev)
@@ -233,15 +234,18 @@ def test_attention_weights(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_decode_attention(dtype):
+@pytest.mark.parametrize("D", [64, 32, 128, 24])
+def test_decode_attention(dtype, D):
+    """Vectorised online-softmax kernel (D = 32/64/128) and the generic
+    fallback (D = 24)."""
     O = ops()
-    H, D, cap, R = 4, 64, 300, 3
+    H, cap, R = 4, 1000, 3
     d = H * D
     kc = torch.randn(R, cap, d, device=dev).to(dtype)
     vc = torch.randn(R, cap, d, device=dev).to(dtype)
     q = torch.randn(5, d, device=dev).to(dtype)
     row_req = torch.tensor([0, 1, 1, 2, 2], dtype=torch.int32, device=dev)
-    nkeys = torch.tensor([1, 17, 18, 300, 64], dtype=torch.int32, device=dev)
+    nkeys = torch.tensor([1, 17, 18, 1000, 64], dtype=torch.int32, device=dev)
     out = torch.empty(5, d, device=dev, dtype=dtype)
     O.attn_decode(q, kc, vc, row_req, nkeys, out, H=H, D=D, row_stride=d, req_stride=cap * d,
                   scale=0.125)
@@ -256,10 +260,10 @@ def test_decode_attention(dtype):
     # scatter
     src = torch.randn(2, d, device=dev).to(dtype)
     O.kv_scatter(src, kc, torch.tensor([2, 0], dtype=torch.int32, device=dev),
-                 torch.tensor([5, 299], dtype=torch.int32, device=dev), row_stride=d,
+                 torch.tensor([5, 999], dtype=torch.int32, device=dev), row_stride=d,
                  req_stride=cap * d)
     torch.cuda.synchronize()
-    assert torch.equal(kc[2, 5], src[0]) and torch.equal(kc[0, 299], src[1])
+    assert torch.equal(kc[2, 5], src[0]) and torch.equal(kc[0, 999], src[1])
 
 
 # ------------------------------------------------------------ layernorm
