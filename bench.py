@@ -167,6 +167,25 @@ def cpu_baseline(args):
                       % (n, B, args.seq, args.tgt)}
 
 
+def _pmc_traffic():
+    """HBM bytes per gemm_bf16_kernel launch (FETCH_SIZE x2 + WRITE_SIZE,
+    launch-weighted over the three layout variants) from the newest committed
+    rocprofv3 PMC summary (profiles/*_train_pmc_traffic.json, written by
+    tools/pmc_traffic.py from tools/profile_round.sh's separate passes)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*_train_pmc_traffic.json")))
+    if not files:
+        return None
+    s = json.load(open(files[-1]))
+    g = [v for k, v in s.items() if k.startswith("gemm_bf16_kernel")]
+    n = sum(v["launches"] for v in g)
+    if not n:
+        return None
+    return {"bytes_per_launch": round(sum(v["hbm_bytes"] * v["launches"] for v in g) / n),
+            "source": os.path.basename(files[-1])}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,7 +238,9 @@ def main():
             g = tr["gemm"]
             roof = {"bound": "mfma", "kernel": "gemm_bf16_kernel (smer_gemm)",
                     "achieved": round(g["tflops"], 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(g["tflops"] / BF16_PEAK_TFLOPS, 4), "traffic": None,
+                    "frac": round(g["tflops"] / BF16_PEAK_TFLOPS, 4), "traffic": (_pmc_traffic() or {}).get("bytes_per_launch"),
+                    "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
+                    "traffic_source": (_pmc_traffic() or {}).get("source"),
                     "avg_launch_us": round(g["avg_us"], 2),
                     "flops_per_launch": g["flops_per_launch"],
                     "share_of_step_time": round(g["share_of_step"], 3)}
