@@ -21,7 +21,18 @@ constexpr int KVB = 64;  // keys (or queries) per LDS tile
 
 template <int D>
 struct AttnCfg {
-  static constexpr int ROWB = D * 2 + 16;            // padded LDS row bytes
+  // D = 64: unpadded 128-B rows with the 16-B chunk index XORed by (row & 7):
+  // conflict-free for both the ds_read_b128 row fragments and the
+  // ds_read_b64_tr_b16 transposed fragments (lane groups per the LDS table
+  // of the gfx950 guide).  Other D: rows padded by 16 B.
+  static constexpr bool SWZ = (D == 64);
+  static constexpr int ROWB = SWZ ? 128 : D * 2 + 16;  // LDS row bytes
+  __device__ static __forceinline__ uint32_t off(int row, int byte) {
+    if constexpr (SWZ)
+      return row * 128 + ((((byte >> 4) ^ (row & 7)) << 4) | (byte & 15));
+    else
+      return row * ROWB + byte;
+  }
   static constexpr int NS = D / 32;                  // 32-deep k-steps over the head dim
   static constexpr int NDT = D / 16;                 // 16-wide head-dim tiles
   static constexpr int CPR = D / 8;                  // 16-B chunks per row
@@ -47,13 +58,13 @@ __device__ __forceinline__ void tile_store(const uint4 (&r)[AttnCfg<D>::CPT], ch
   for (int c = 0; c < AttnCfg<D>::CPT; ++c) {
     int i = tid + 256 * c;
     int row = i / AttnCfg<D>::CPR, ch = i % AttnCfg<D>::CPR;
-    *reinterpret_cast<uint4*>(buf + row * AttnCfg<D>::ROWB + ch * 16) = r[c];
+    *reinterpret_cast<uint4*>(buf + AttnCfg<D>::off(row, ch * 16)) = r[c];
   }
 }
 // Row fragment: rows rbase+c16, head-dim k-step s (8 contiguous elements).
 template <int D>
 __device__ __forceinline__ bf16x8 row_frag(const char* buf, int rbase, int s, int lane) {
-  return lds_read_b128(buf, (rbase + (lane & 15)) * AttnCfg<D>::ROWB + (s * 32 + 8 * (lane >> 4)) * 2);
+  return lds_read_b128(buf, AttnCfg<D>::off(rbase + (lane & 15), (s * 32 + 8 * (lane >> 4)) * 2));
 }
 // Transposed fragment for the 32-row step ks over head-dim tile dt: element
 // j of lane-group g = row ks*32 + (j<4 ? 4g+j : 16+4g+j-4), column dt*16+c16.
@@ -61,8 +72,8 @@ template <int D>
 __device__ __forceinline__ bf16x8 tr_frag(const char* buf, int ks, int dt, int lane) {
   int g = lane >> 4, c16 = lane & 15, qq = c16 >> 2, pp = c16 & 3;
   int col = (dt * 16 + 4 * pp) * 2;
-  bf16x4 lo = lds_read_tr16(buf, (ks * 32 + 4 * g + qq) * AttnCfg<D>::ROWB + col);
-  bf16x4 hi = lds_read_tr16(buf, (ks * 32 + 16 + 4 * g + qq) * AttnCfg<D>::ROWB + col);
+  bf16x4 lo = lds_read_tr16(buf, AttnCfg<D>::off(ks * 32 + 4 * g + qq, col));
+  bf16x4 hi = lds_read_tr16(buf, AttnCfg<D>::off(ks * 32 + 16 + 4 * g + qq, col));
   return cat4(lo, hi);
 }
 __device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
@@ -79,8 +90,11 @@ __device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
 // ---------------------------------------------------------------------------
 // bf16 forward
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
+// QG query groups of 16 per wave (block = 64*QG queries): K / V fragments
+// read from LDS once per wave feed QG groups, halving LDS traffic per MFMA
+// at QG = 2 (the forward is otherwise LDS-bandwidth co-limited).
+template <int D, int QG, bool DROP>
+__global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
                                                      const bf16* __restrict__ q, long ldq,
                                                      const bf16* __restrict__ k, long ldk,
                                                      const bf16* __restrict__ v, long ldv,
@@ -90,23 +104,28 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
                                                      float scale, uint32_t drop_thr, uint32_t seed,
                                                      float drop_scale) {
   using C = AttnCfg<D>;
+  constexpr int QB = 64 * QG;  // queries per block
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
+  // per-key additive score bias of the staged tile: 0, or -inf for padded /
+  // out-of-range keys; it seeds the S accumulators, so masking costs no VALU
+  __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
   xcd_block2d(BX, BY);
   const int bh = BY, b = bh / H, h = bh % H;
-  const int qi = BX * 64 + wave * 16 + c16;
-  const bool qvalid = qi < Lq;
+  const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
 
-  bf16x8 qf[C::NS];
-  {
+  bf16x8 qf[QG][C::NS];
+#pragma unroll
+  for (int gq = 0; gq < QG; ++gq) {
+    const int qi = q0w + gq * 16 + c16;
     const bf16* qrow = q + (long)(b * Lq + min(qi, Lq - 1)) * ldq + h * D;
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(qrow + s * 32 + 8 * g);
-      if (!qvalid) qf[s] = bf16x8{};
+      qf[gq][s] = *reinterpret_cast<const bf16x8*>(qrow + s * 32 + 8 * g);
+      if (qi >= Lq) qf[gq][s] = bf16x8{};
     }
   }
   const bf16* kb = k + (long)b * Lk * ldk + h * D;
@@ -115,118 +134,149 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16(int B, int H, int Lq, int L
 
   int n_tiles = (Lk + KVB - 1) / KVB;
   if (causal) {
-    int qmax = min(Lq, BX * 64 + 64);
+    int qmax = min(Lq, BX * QB + QB);
     n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
   }
-  float m_run = -INFINITY, l_run = 0.f;
-  f32x4 acc[C::NDT];
+  float m_run[QG], l_run[QG];
+  uint32_t rowkey[QG];
+  f32x4 acc[QG][C::NDT];
 #pragma unroll
-  for (int i = 0; i < C::NDT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int gq = 0; gq < QG; ++gq) {
+    rowkey[gq] = DROP ? smer_rowkey(seed, (uint32_t)(bh * Lq + q0w + gq * 16 + c16)) : 0u;
+    m_run[gq] = -INFINITY;
+    l_run[gq] = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::NDT; ++i) acc[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   uint4 rk[C::CPT], rv[C::CPT];
+  auto key_bias = [&](int key) -> float {
+    return (key >= Lk || (kp && kp[key])) ? -INFINITY : 0.f;
+  };
   if (n_tiles > 0) {
     tile_load<D>(rk, kb, ldk, 0, Lk, tid);
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
+    if (tid < KVB) kbias[0][tid] = key_bias(tid);
   }
   __syncthreads();
-  const uint32_t qrow_id = (uint32_t)(bh * Lq + qi);
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
+    float nbias = 0.f;
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
+      if (tid < KVB) nbias = key_bias((t + 1) * KVB + tid);
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
-    f32x4 st[4];
+    f32x4 st[QG][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      st[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
 #pragma unroll
-      for (int s = 0; s < C::NS; ++s) st[mt] = mfma16(row_frag<D>(Ks, mt * 16, s, lane), qf[s], st[mt]);
-    }
-    float x[4][4];
-    float tmax = -INFINITY;
-    // padded / out-of-range keys of this tile as one wave-uniform bitmask
-    const int kl = t * KVB + lane;
-    const unsigned long long kbad = __ballot(kl >= Lk || (kp && kp[min(kl, Lk - 1)]));
-    const int q0w = BX * 64 + wave * 16;
-    if (kbad != 0ull || (causal && t * KVB + KVB - 1 > q0w)) {
+      for (int gq = 0; gq < QG; ++gq) st[gq][mt] = kbv;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
+      for (int s = 0; s < C::NS; ++s) {
+        const bf16x8 kf = row_frag<D>(Ks, mt * 16, s, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int kk = mt * 16 + 4 * g + r;
-          const bool ok = !((kbad >> kk) & 1ull) && (!causal || t * KVB + kk <= qi);
-          const float xv = ok ? st[mt][r] * c : -INFINITY;
-          x[mt][r] = xv;
-          tmax = fmaxf(tmax, xv);
-        }
-    } else {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          x[mt][r] = st[mt][r] * c;
-          tmax = fmaxf(tmax, x[mt][r]);
-        }
-    }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
-    l_run *= alpha;
-#pragma unroll
-    for (int i = 0; i < C::NDT; ++i) acc[i] *= alpha;
-    float p[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = exp2f(x[mt][r] - m_use);
-        l_run += pv;
-        if (drop_thr) {
-          int key = t * KVB + mt * 16 + 4 * g + r;
-          pv = smer_keep(seed, drop_thr, qrow_id, (uint32_t)key) ? pv * drop_scale : 0.f;
-        }
-        p[mt][r] = pv;
+        for (int gq = 0; gq < QG; ++gq) st[gq][mt] = mfma16(kf, qf[gq][s], st[gq][mt]);
       }
-    m_run = m_new;
+    }
+    bf16x8 pf[QG][2];
+#pragma unroll
+    for (int gq = 0; gq < QG; ++gq) {
+      const int qi = q0w + gq * 16 + c16;
+      // max in raw score units (c > 0), exponent as one fma: p = 2^(s*c - m*c)
+      if (causal && t * KVB + KVB - 1 > q0w + gq * 16) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t * KVB + mt * 16 + 4 * g + r > qi) st[gq][mt][r] = -INFINITY;
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, st[gq][mt][r]);
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float m_new = fmaxf(m_run[gq], tmax);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      // lazy rescale: skip the accumulator multiply while no lane's max moved
+      if (__ballot(m_new > m_run[gq]) != 0ull) {
+        const float alpha = fast_exp2((m_run[gq] - m_use) * c);
+        l_run[gq] *= alpha;
+#pragma unroll
+        for (int i = 0; i < C::NDT; ++i) acc[gq][i] *= alpha;
+      }
+      const float mc = m_use * c;
+      float p[4][4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[mt][r] = fast_exp2(fmaf(st[gq][mt][r], c, -mc));
+          l_run[gq] += p[mt][r];
+        }
+      if (DROP) {
+        // keys mt*16+4g+{0,1} and {2,3} share one hash
+        const uint32_t pb = (uint32_t)(t * (KVB / 2) + 2 * g);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hb = smer_pair_bits(rowkey[gq], pb + mt * 8 + rp);
+            p[mt][2 * rp] = (hb & 0xFFFFu) >= drop_thr ? p[mt][2 * rp] * drop_scale : 0.f;
+            p[mt][2 * rp + 1] = (hb >> 16) >= drop_thr ? p[mt][2 * rp + 1] * drop_scale : 0.f;
+          }
+      }
+      m_run[gq] = m_new;
+      pf[gq][0] = pack_p(p, 0);
+      pf[gq][1] = pack_p(p, 1);
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pf = pack_p(p, ks);
 #pragma unroll
-      for (int dt = 0; dt < C::NDT; ++dt) acc[dt] = mfma16(tr_frag<D>(Vs, ks, dt, lane), pf, acc[dt]);
+      for (int dt = 0; dt < C::NDT; ++dt) {
+        const bf16x8 vf = tr_frag<D>(Vs, ks, dt, lane);
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) acc[gq][dt] = mfma16(vf, pf[gq][ks], acc[gq][dt]);
+      }
     }
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
+      if (tid < KVB) kbias[cur ^ 1][tid] = nbias;
     }
     __syncthreads();
   }
-  float l = l_run + __shfl_xor(l_run, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (!qvalid) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  bf16* orow = o + (long)(b * Lq + qi) * ldo + h * D;
 #pragma unroll
-  for (int dt = 0; dt < C::NDT; ++dt) {
-    bf16x4 w;
+  for (int gq = 0; gq < QG; ++gq) {
+    const int qi = q0w + gq * 16 + c16;
+    float l = l_run[gq] + __shfl_xor(l_run[gq], 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qi >= Lq) continue;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16* orow = o + (long)(b * Lq + qi) * ldo + h * D;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[dt][r] * inv);
-    *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
+    for (int dt = 0; dt < C::NDT; ++dt) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[gq][dt][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
+    }
+    if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_run[gq] * c + log2f(l)) * LN2_F : INFINITY;
   }
-  if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_run + log2f(l)) * LN2_F : INFINITY;
 }
 
 // ---------------------------------------------------------------------------
 // bf16 backward: dK / dV
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
@@ -236,13 +286,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     bf16* __restrict__ dv, long lddv) {
   using C = AttnCfg<D>;
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
-  __shared__ float s_lse[2][KVB], s_del[2][KVB];
+  // per query of the staged tile: lse (log2 units; +inf past Lq so P = 0),
+  // delta, and the dropout row key
+  __shared__ __attribute__((aligned(16))) float s_lse[2][KVB];
+  __shared__ __attribute__((aligned(16))) float s_del[2][KVB];
+  __shared__ __attribute__((aligned(16))) uint32_t s_rk[2][KVB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
   xcd_block2d(BX, BY);
   const int bh = BY, b = bh / H, h = bh % H;
   const int kj = BX * 64 + wave * 16 + c16;
+  // padded keys get no gradient: their dK / dV rows are written as zeros
   const bool kvalid = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
   const float c = scale * LOG2E_F;
 
@@ -253,13 +308,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     for (int s = 0; s < C::NS; ++s) {
       kf[s] = *reinterpret_cast<const bf16x8*>(k + row * ldk + h * D + s * 32 + 8 * g);
       vf[s] = *reinterpret_cast<const bf16x8*>(v + row * ldv + h * D + s * 32 + 8 * g);
-      if (kj >= Lk) { kf[s] = bf16x8{}; vf[s] = bf16x8{}; }
     }
   }
   const bf16* qb = q + (long)b * Lq * ldq + h * D;
   const bf16* ob = dout + (long)b * Lq * lddo + h * D;
   const float* lb = lse + (long)bh * Lq;
   const float* db = delta + (long)bh * Lq;
+  const uint32_t kpair = (uint32_t)kj >> 1;
+  const bool khi = kj & 1;
 
   const int n_qt = (Lq + KVB - 1) / KVB;
   const int t0 = causal ? min(n_qt, (BX * 64) / KVB) : 0;
@@ -269,6 +325,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
 
   uint4 rq[C::CPT], ro[C::CPT];
   float rl = 0.f, rd = 0.f;
+  uint32_t rr = 0u;
   auto load = [&](int t) {
     tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
     tile_load<D>(ro, ob, lddo, t * KVB, Lq, tid);
@@ -276,12 +333,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
       int qq = t * KVB + tid;
       rl = qq < Lq ? lb[qq] * LOG2E_F : INFINITY;
       rd = qq < Lq ? db[qq] : 0.f;
+      if (DROP) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
     }
   };
   auto store = [&](int buf) {
     tile_store<D>(rq, sm[buf][0], tid);
     tile_store<D>(ro, sm[buf][1], tid);
-    if (tid < KVB) { s_lse[buf][tid] = rl; s_del[buf][tid] = rd; }
+    if (tid < KVB) {
+      s_lse[buf][tid] = rl;
+      s_del[buf][tid] = rd;
+      if (DROP) s_rk[buf][tid] = rr;
+    }
   };
   if (t0 < n_qt) { load(t0); store(0); }
   __syncthreads();
@@ -291,6 +353,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     if (more) load(t + 1);
     const char* Qs = sm[cur][0];
     const char* Os = sm[cur][1];
+    const bool diag = causal && t * KVB < BX * 64 + 64;
     float pd[4][4], ds[4][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -300,21 +363,22 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
         sacc = mfma16(row_frag<D>(Qs, mt * 16, s, lane), kf[s], sacc);
         dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[s], dpacc);
       }
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int ql = mt * 16 + 4 * g + r;
-        int qq = t * KVB + ql;
-        bool ok = qq < Lq && kvalid && (!causal || kj <= qq);
-        float pv = ok ? exp2f(sacc[r] * c - s_lse[cur][ql]) : 0.f;
+        float pv = fast_exp2(fmaf(sacc[r], c, -l4[r]));
+        if (diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
         float dpv = dpacc[r];
         float pdv = pv;
-        if (drop_thr) {
-          bool keep = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qq), (uint32_t)kj);
+        if (DROP) {
+          const uint32_t hb = smer_pair_bits(s_rk[cur][mt * 16 + 4 * g + r], kpair);
+          const bool keep = (khi ? (hb >> 16) : (hb & 0xFFFFu)) >= drop_thr;
           pdv = keep ? pv * drop_scale : 0.f;
           dpv = keep ? dpv * drop_scale : 0.f;
         }
         pd[mt][r] = pdv;
-        ds[mt][r] = pv * (dpv - s_del[cur][ql]);
+        ds[mt][r] = pv * (dpv - d4[r]);
       }
     }
 #pragma unroll
@@ -333,11 +397,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
   if (kj >= Lk) return;
   bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
   bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
+  const float ks_ = kvalid ? scale : 0.f, vs_ = kvalid ? 1.f : 0.f;
 #pragma unroll
   for (int dt = 0; dt < C::NDT; ++dt) {
     bf16x4 wk, wv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(adk[dt][r] * scale); wv[r] = (bf16)adv[dt][r]; }
+    for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(adk[dt][r] * ks_); wv[r] = (bf16)(adv[dt][r] * vs_); }
     *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
     *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
   }
@@ -346,7 +411,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
 // ---------------------------------------------------------------------------
 // bf16 backward: dQ
 // ---------------------------------------------------------------------------
-template <int D>
+template <int D, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
@@ -355,6 +420,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq) {
   using C = AttnCfg<D>;
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
+  __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
@@ -370,14 +436,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     for (int s = 0; s < C::NS; ++s) {
       qf[s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
       of[s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
-      if (!qvalid) { qf[s] = bf16x8{}; of[s] = bf16x8{}; }
     }
   }
+  // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
   const float lse2 = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
   const float dlt = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
+  const uint32_t rowkey = DROP ? smer_rowkey(seed, (uint32_t)(bh * Lq + qi)) : 0u;
   const bf16* kb = k + (long)b * Lk * ldk + h * D;
   const bf16* vb = v + (long)b * Lk * ldv + h * D;
   const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  auto key_bias = [&](int key) -> float {
+    return (key >= Lk || (kp && kp[key])) ? -INFINITY : 0.f;
+  };
   int n_tiles = (Lk + KVB - 1) / KVB;
   if (causal) {
     int qmax = min(Lq, BX * 64 + 64);
@@ -392,39 +462,48 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
+    if (tid < KVB) kbias[0][tid] = key_bias(tid);
   }
   __syncthreads();
-  const uint32_t qrow_id = (uint32_t)(bh * Lq + qi);
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
+    float nbias = 0.f;
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
+      if (tid < KVB) nbias = key_bias((t + 1) * KVB + tid);
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
+    const bool diag = causal && t * KVB + KVB - 1 > BX * 64 + wave * 16;
     float ds[4][4];
-    const int kl = t * KVB + lane;
-    const unsigned long long kbad = __ballot(kl >= Lk || (kp && kp[min(kl, Lk - 1)]));
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
+      f32x4 sacc = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
+      f32x4 dpacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < C::NS; ++s) {
         sacc = mfma16(row_frag<D>(Ks, mt * 16, s, lane), qf[s], sacc);
         dpacc = mfma16(row_frag<D>(Vs, mt * 16, s, lane), of[s], dpacc);
       }
+      float dpv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dpv[r] = dpacc[r];
+      if (DROP) {
+        const uint32_t pb = (uint32_t)(t * (KVB / 2) + mt * 8 + 2 * g);
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp) {
+          const uint32_t hb = smer_pair_bits(rowkey, pb + rp);
+          dpv[2 * rp] = (hb & 0xFFFFu) >= drop_thr ? dpv[2 * rp] * drop_scale : 0.f;
+          dpv[2 * rp + 1] = (hb >> 16) >= drop_thr ? dpv[2 * rp + 1] * drop_scale : 0.f;
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int kk = mt * 16 + 4 * g + r;
-        const int key = t * KVB + kk;
-        const bool ok = qvalid && !((kbad >> kk) & 1ull) && (!causal || key <= qi);
-        float pv = ok ? exp2f(sacc[r] * c - lse2) : 0.f;
-        float dpv = dpacc[r];
-        if (drop_thr)
-          dpv = smer_keep(seed, drop_thr, qrow_id, (uint32_t)key) ? dpv * drop_scale : 0.f;
-        ds[mt][r] = pv * (dpv - dlt);
+        float pv = fast_exp2(fmaf(sacc[r], c, -lse2));
+        if (diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
+        ds[mt][r] = pv * (dpv[r] - dlt);
       }
     }
 #pragma unroll
@@ -436,6 +515,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
+      if (tid < KVB) kbias[cur ^ 1][tid] = nbias;
     }
     __syncthreads();
   }
@@ -554,7 +634,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int B, int H, int Lq, int Lk
   for (int j = lane; j < Lk; j += 64) {
     float e = expf(sc[j] - mu);
     sum += e;
-    if (drop_thr) e = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qi), (uint32_t)j) ? e * drop_scale : 0.f;
+    if (drop_thr) e = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j) ? e * drop_scale : 0.f;
     sc[j] = e;
   }
   sum = wave_sum(sum);
@@ -595,7 +675,7 @@ __global__ void attn_bwd_ps_f32(int B, int H, int Lq, int Lk, int D, const float
   }
   float pd = p;
   if (drop_thr) {
-    bool keep = smer_keep(seed, drop_thr, (uint32_t)(bh * Lq + qi), (uint32_t)j);
+    bool keep = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j);
     pd = keep ? p * drop_scale : 0.f;
     dp = keep ? dp * drop_scale : 0.f;
   }
@@ -863,8 +943,12 @@ static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                             long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
                             const uint8_t* kpm, int causal, float scale, uint32_t thr,
                             uint32_t seed, float ds, hipStream_t s) {
-  dim3 grid((Lq + 63) / 64, B * H);
-  hipLaunchKernelGGL(attn_fwd_bf16<D>, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
+  // two query groups per wave once there are enough blocks to fill the chip
+  const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
+  dim3 grid(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H);
+  auto kern = qg2 ? (thr ? attn_fwd_bf16<D, 2, true> : attn_fwd_bf16<D, 2, false>)
+                  : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
                      scale, thr, seed, ds);
 }
@@ -878,8 +962,8 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
   if (Lq == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_drop_threshold(drop_p);
-  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  uint32_t thr = smer_attn_threshold(drop_p);
+  float ds = smer_attn_scale(thr);
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
@@ -913,11 +997,13 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                             const float* lse, const float* delta, const uint8_t* kpm, int causal,
                             float scale, uint32_t thr, uint32_t seed, float ds, void* dq,
                             long lddq, void* dk, long lddk, void* dv, long lddv, hipStream_t s) {
-  hipLaunchKernelGGL(attn_bwd_dkdv_bf16<D>, dim3((Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+  auto kdkdv = thr ? attn_bwd_dkdv_bf16<D, true> : attn_bwd_dkdv_bf16<D, false>;
+  auto kdq = thr ? attn_bwd_dq_bf16<D, true> : attn_bwd_dq_bf16<D, false>;
+  hipLaunchKernelGGL(kdkdv, dim3((Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
                      (bf16*)dk, lddk, (bf16*)dv, lddv);
-  hipLaunchKernelGGL(attn_bwd_dq_bf16<D>, dim3((Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+  hipLaunchKernelGGL(kdq, dim3((Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
                      (bf16*)dq, lddq);
@@ -935,8 +1021,8 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
                "smer_attn_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_drop_threshold(drop_p);
-  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  uint32_t thr = smer_attn_threshold(drop_p);
+  float ds = smer_attn_scale(thr);
   float* delta = (float*)workspace;
   long nrow = (long)B * H * Lq;
   if (dtype == SMER_BF16) {

@@ -30,6 +30,10 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
+// Raw v_exp_f32 (2^x; -inf -> 0, no denormal range fix-up): the softmax
+// exponents are <= 0 so the fix-up libm's exp2f adds is dead weight.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -57,6 +61,35 @@ static inline uint32_t smer_drop_threshold(float p) {
   if (p <= 0.f) return 0u;
   double t = (double)p * 4294967296.0;
   return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+}
+
+// Attention-probability dropout (a separate stream from smer_keep): one
+// 32-bit hash per (query row, key pair) feeds 16 bits to each of the two
+// keys, keep iff bits >= thr16 = round(p * 65536); survivors are scaled by
+// 65536 / (65536 - thr16) (exactly unbiased for the realised rate).  The
+// per-row key is hashed once per row, so a key costs half a hash in the
+// forward / dQ loops.  numpy mirror: tests/hashref.py attn_keep_mask.
+__device__ __forceinline__ uint32_t smer_mix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t smer_rowkey(uint32_t seed, uint32_t row) {
+  return smer_mix32(smer_mix32(row ^ 0x85EBCA6Bu) ^ seed);
+}
+__device__ __forceinline__ uint32_t smer_pair_bits(uint32_t rowkey, uint32_t pair) {
+  return smer_mix32(rowkey + pair * 0x9E3779B9u);
+}
+__device__ __forceinline__ bool smer_attn_keep(uint32_t rowkey, uint32_t thr16, uint32_t key) {
+  const uint32_t h = smer_pair_bits(rowkey, key >> 1);
+  return ((key & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr16;
+}
+static inline uint32_t smer_attn_threshold(float p) {
+  if (p <= 0.f) return 0u;
+  long t = (long)((double)p * 65536.0 + 0.5);
+  return (uint32_t)(t < 1 ? 1 : (t > 65535 ? 65535 : t));
+}
+static inline float smer_attn_scale(uint32_t thr16) {
+  return thr16 ? (float)(65536.0 / (65536.0 - (double)thr16)) : 1.f;
 }
 
 // out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order

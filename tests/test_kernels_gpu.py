@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.hashref import keep_mask
+from tests.hashref import attn_keep_mask, attn_scale, keep_mask
 
 pytestmark = pytest.mark.gpu
 
@@ -123,6 +123,8 @@ def test_gemm_epilogue(dtype, M, N, K):
 
 # ------------------------------------------------------------ attention
 def attn_ref(q, k, v, B, H, Lq, Lk, D, kpm, causal, scale, keep=None, p=0.0):
+    """fp32 reference; dropout survivors scaled by the kernel's 16-bit-rate
+    factor (tests/hashref.py attn_scale)."""
     qh = q.float().view(B, Lq, H, D).transpose(1, 2)
     kh = k.float().view(B, Lk, H, D).transpose(1, 2)
     vh = v.float().view(B, Lk, H, D).transpose(1, 2)
@@ -136,7 +138,7 @@ def attn_ref(q, k, v, B, H, Lq, Lk, D, kpm, causal, scale, keep=None, p=0.0):
     lse = torch.logsumexp(s, -1)
     pr = torch.softmax(s, -1)
     if keep is not None:
-        pr = torch.where(keep, pr / (1 - p), torch.zeros_like(pr))
+        pr = torch.where(keep, pr * attn_scale(p), torch.zeros_like(pr))
     o = (pr @ vh).transpose(1, 2).reshape(B * Lq, H * D)
     return o, lse
 
@@ -184,20 +186,25 @@ def test_attention_fwd_bwd(dtype, D, Lq, Lk, causal, pad):
     assert rel_err(dv, vf.grad) < tolb
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_attention_dropout(dtype):
+@pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
+                                                 (torch.float32, 2, 2, 96, True),
+                                                 (torch.bfloat16, 16, 8, 512, False),
+                                                 (torch.bfloat16, 16, 8, 512, True)])
+def test_attention_dropout(dtype, B, H, L, causal):
+    """Dropout mask = tests/hashref.attn_keep_mask; the large shapes take the
+    two-query-group forward (>= 512 workgroups)."""
     O = ops()
-    B, H, L, D = 2, 2, 96, 64
+    D = 64
     p, seed = 0.1, 77
     q, k, v, kpm = _attn_inputs(B, H, L, L, D, dtype, True)
     scale = 0.125
-    keep = torch.from_numpy(keep_mask(seed, p, B * H * L, L)).to(dev).view(B, H, L, L)
+    keep = torch.from_numpy(attn_keep_mask(seed, p, B * H * L, L)).to(dev).view(B, H, L, L)
     o = torch.empty(B * L, H * D, device=dev, dtype=dtype)
     lse = torch.empty(B, H, L, device=dev)
-    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=True, scale=scale,
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal, scale=scale,
                drop_p=p, seed=seed)
     qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, k, v))
-    ro, _ = attn_ref(qf, kf, vf, B, H, L, L, D, kpm, True, scale, keep, p)
+    ro, _ = attn_ref(qf, kf, vf, B, H, L, L, D, kpm, causal, scale, keep, p)
     torch.cuda.synchronize()
     tol = 2e-2 if dtype == torch.bfloat16 else 2e-5
     assert rel_err(o, ro) < tol
@@ -206,7 +213,7 @@ def test_attention_dropout(dtype):
     dq = torch.empty_like(q)
     dk = torch.empty_like(k.contiguous())
     dv = torch.empty_like(dk)
-    O.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=True,
+    O.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal,
                scale=scale, drop_p=p, seed=seed)
     torch.cuda.synchronize()
     tolb = 4e-2 if dtype == torch.bfloat16 else 1e-4

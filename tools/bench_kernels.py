@@ -86,9 +86,12 @@ def bench_attn():
         dkv = torch.empty_like(kv)
         tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dkv[:, :H * D], dkv[:, H * D:],
                                          B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=sc))
+        tbd = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dkv[:, :H * D], dkv[:, H * D:],
+                                          B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=sc,
+                                          drop_p=0.1, seed=1))
         fl = 4.0 * B * H * Lq * Lk * D * (0.5 if causal else 1.0)
         print("%-9s fwd %8.1f us %6.1f TF | fwd+drop %8.1f us | bwd %8.1f us %6.1f TF (2.5x fwd flops)"
-              % (name, t, fl / t / 1e6, td, tb, 2.5 * fl / tb / 1e6))
+              " | bwd+drop %8.1f us" % (name, t, fl / t / 1e6, td, tb, 2.5 * fl / tb / 1e6, tbd))
 
 
 if __name__ == "__main__":
