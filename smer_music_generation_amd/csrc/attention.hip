@@ -397,12 +397,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
   if (kj >= Lk) return;
   bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
   bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
-  const float ks_ = kvalid ? scale : 0.f, vs_ = kvalid ? 1.f : 0.f;
+  // select, not multiply: a padded key's unmasked P may have overflowed
 #pragma unroll
   for (int dt = 0; dt < C::NDT; ++dt) {
     bf16x4 wk, wv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { wk[r] = (bf16)(adk[dt][r] * ks_); wv[r] = (bf16)(adv[dt][r] * vs_); }
+    for (int r = 0; r < 4; ++r) {
+      wk[r] = (bf16)(kvalid ? adk[dt][r] * scale : 0.f);
+      wv[r] = (bf16)(kvalid ? adv[dt][r] : 0.f);
+    }
     *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
     *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
   }

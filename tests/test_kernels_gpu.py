@@ -186,6 +186,33 @@ def test_attention_fwd_bwd(dtype, D, Lq, Lk, causal, pad):
     assert rel_err(dv, vf.grad) < tolb
 
 
+@pytest.mark.parametrize("D", [32, 64])
+def test_attention_padded_keys_with_huge_scores(D):
+    """Padded keys whose raw scores dwarf the valid ones: they must not leak
+    into O (forward) nor produce inf/NaN in dK/dV (their rows are zero)."""
+    O = ops()
+    B, H, L = 2, 2, 128
+    q, k, v, kpm = _attn_inputs(B, H, L, L, D, torch.bfloat16, True)
+    k = k.clone()
+    pad = kpm.bool().view(B, L).repeat_interleave(1, 0)
+    kk = k.view(B, L, H * D)
+    kk[pad] = (q.view(B, L, H * D)[pad].float() * 60.0).to(torch.bfloat16)
+    o = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=False, scale=0.125)
+    do = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(k)
+    O.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=False,
+               scale=0.125, drop_p=0.1, seed=3)
+    torch.cuda.synchronize()
+    for t in (o, dq, dk, dv):
+        assert torch.isfinite(t.float()).all()
+    assert (dk.view(B, L, -1)[pad] == 0).all() and (dv.view(B, L, -1)[pad] == 0).all()
+    qf, kf, vf = (t.float() for t in (q, k, v))
+    ro, _ = attn_ref(qf, kf, vf, B, H, L, L, D, kpm, False, 0.125)
+    assert rel_err(o, ro) < 2e-2
+
+
 @pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
                                                  (torch.float32, 2, 2, 96, True),
                                                  (torch.bfloat16, 16, 8, 512, False),
