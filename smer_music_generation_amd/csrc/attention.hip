@@ -637,7 +637,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int B, int H, int Lq, int Lk
   for (int j = lane; j < Lk; j += 64) {
     float e = expf(sc[j] - mu);
     sum += e;
-    if (drop_thr) e = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j) ? e * drop_scale : 0.f;
+    if (drop_thr) e = smer_keep16(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j) ? e * drop_scale : 0.f;
     sc[j] = e;
   }
   sum = wave_sum(sum);
@@ -678,7 +678,7 @@ __global__ void attn_bwd_ps_f32(int B, int H, int Lq, int Lk, int D, const float
   }
   float pd = p;
   if (drop_thr) {
-    bool keep = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j);
+    bool keep = smer_keep16(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j);
     pd = keep ? p * drop_scale : 0.f;
     dp = keep ? dp * drop_scale : 0.f;
   }
@@ -965,8 +965,8 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
   if (Lq == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_attn_threshold(drop_p);
-  float ds = smer_attn_scale(thr);
+  uint32_t thr = smer_drop_thr16(drop_p);
+  float ds = smer_drop_scale16(thr);
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
@@ -1024,8 +1024,8 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
                "smer_attn_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_attn_threshold(drop_p);
-  float ds = smer_attn_scale(thr);
+  uint32_t thr = smer_drop_thr16(drop_p);
+  float ds = smer_drop_scale16(thr);
   float* delta = (float*)workspace;
   long nrow = (long)B * H * Lq;
   if (dtype == SMER_BF16) {

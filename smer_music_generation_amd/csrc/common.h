@@ -45,30 +45,13 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Counter-based dropout hash: keep iff hash(seed, row, col) >= threshold,
-// threshold = p * 2^32.  Same function in every forward/backward site.
-__device__ __forceinline__ uint32_t smer_hash3(uint32_t seed, uint32_t a, uint32_t b) {
-  uint32_t h = seed ^ 0x9E3779B9u;
-  h ^= a * 0xCC9E2D51u; h = (h << 15) | (h >> 17); h *= 0x1B873593u;
-  h ^= b * 0x85EBCA6Bu; h = (h << 13) | (h >> 19); h = h * 5u + 0xE6546B64u;
-  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-  return h;
-}
-__device__ __forceinline__ bool smer_keep(uint32_t seed, uint32_t thr, uint32_t a, uint32_t b) {
-  return smer_hash3(seed, a, b) >= thr;
-}
-static inline uint32_t smer_drop_threshold(float p) {
-  if (p <= 0.f) return 0u;
-  double t = (double)p * 4294967296.0;
-  return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-}
-
-// Attention-probability dropout (a separate stream from smer_keep): one
-// 32-bit hash per (query row, key pair) feeds 16 bits to each of the two
-// keys, keep iff bits >= thr16 = round(p * 65536); survivors are scaled by
-// 65536 / (65536 - thr16) (exactly unbiased for the realised rate).  The
-// per-row key is hashed once per row, so a key costs half a hash in the
-// forward / dQ loops.  numpy mirror: tests/hashref.py attn_keep_mask.
+// Dropout (every site: activations, attention probabilities, LN / embedding
+// gradients).  Counter-based: one 32-bit hash per (row, column pair) feeds
+// 16 bits to each of the two columns; keep iff bits >= thr16 =
+// round(p * 65536); survivors are scaled by 65536 / (65536 - thr16), exactly
+// unbiased for the realised rate.  The per-row key is hashed once per row,
+// so a column costs half a hash (2 multiplies per pair).  numpy mirror:
+// tests/hashref.py keep_mask.
 __device__ __forceinline__ uint32_t smer_mix32(uint32_t h) {
   h ^= h >> 16; h *= 0x7FEB352Du; h ^= h >> 15; h *= 0x846CA68Bu; h ^= h >> 16;
   return h;
@@ -79,16 +62,26 @@ __device__ __forceinline__ uint32_t smer_rowkey(uint32_t seed, uint32_t row) {
 __device__ __forceinline__ uint32_t smer_pair_bits(uint32_t rowkey, uint32_t pair) {
   return smer_mix32(rowkey + pair * 0x9E3779B9u);
 }
-__device__ __forceinline__ bool smer_attn_keep(uint32_t rowkey, uint32_t thr16, uint32_t key) {
-  const uint32_t h = smer_pair_bits(rowkey, key >> 1);
-  return ((key & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr16;
+__device__ __forceinline__ bool smer_keep16(uint32_t rowkey, uint32_t thr16, uint32_t col) {
+  const uint32_t h = smer_pair_bits(rowkey, col >> 1);
+  return ((col & 1u) ? (h >> 16) : (h & 0xFFFFu)) >= thr16;
 }
-static inline uint32_t smer_attn_threshold(float p) {
+// 8 consecutive columns starting at an even col0: v[i] = keep ? v[i] * ds : 0
+__device__ __forceinline__ void smer_drop8(uint32_t rowkey, uint32_t thr16, float ds, uint32_t col0,
+                                           float (&v)[8]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t h = smer_pair_bits(rowkey, (col0 >> 1) + k);
+    v[2 * k] = (h & 0xFFFFu) >= thr16 ? v[2 * k] * ds : 0.f;
+    v[2 * k + 1] = (h >> 16) >= thr16 ? v[2 * k + 1] * ds : 0.f;
+  }
+}
+static inline uint32_t smer_drop_thr16(float p) {
   if (p <= 0.f) return 0u;
   long t = (long)((double)p * 65536.0 + 0.5);
   return (uint32_t)(t < 1 ? 1 : (t > 65535 ? 65535 : t));
 }
-static inline float smer_attn_scale(uint32_t thr16) {
+static inline float smer_drop_scale16(uint32_t thr16) {
   return thr16 ? (float)(65536.0 / (65536.0 - (double)thr16)) : 1.f;
 }
 

@@ -40,7 +40,7 @@ __device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int ro
   float v = acc * e.alpha;
   if (e.bias) v += e.bias[col];
   if (e.relu) v = fmaxf(v, 0.f);
-  if (e.drop_thr) v = smer_keep(e.seed, e.drop_thr, (uint32_t)row, (uint32_t)col) ? v * e.drop_scale : 0.f;
+  if (e.drop_thr) v = smer_keep16(smer_rowkey(e.seed, (uint32_t)row), e.drop_thr, (uint32_t)col) ? v * e.drop_scale : 0.f;
   if (e.residual) v += to_f32(((const T*)e.residual)[(long)row * e.ldr + col]);
   if (e.gate) {
     float gv = to_f32(((const T*)e.gate)[(long)row * e.ldg + col]);
@@ -75,11 +75,7 @@ __device__ __forceinline__ void epi_apply8(const GemmEpi& e, int M, int N, int r
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
   }
-  if (e.drop_thr) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      v[k] = smer_keep(e.seed, e.drop_thr, (uint32_t)row, (uint32_t)(col + k)) ? v[k] * e.drop_scale : 0.f;
-  }
+  if (e.drop_thr) smer_drop8(smer_rowkey(e.seed, (uint32_t)row), e.drop_thr, e.drop_scale, (uint32_t)col, v);
   if (e.residual) {
     const bf16x8 r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)row * e.ldr + col);
 #pragma unroll
@@ -512,8 +508,8 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
   GemmEpi e;
   e.bias = bias; e.alpha = alpha; e.relu = relu; e.residual = residual; e.ldr = ldr;
   e.gate = gate; e.ldg = ldg; e.gate_scale = gate_scale;
-  e.drop_thr = smer_drop_threshold(drop_p); e.seed = drop_seed;
-  e.drop_scale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  e.drop_thr = smer_drop_thr16(drop_p); e.seed = drop_seed;
+  e.drop_scale = smer_drop_scale16(e.drop_thr);
   e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf; e.accumulate = accumulate;
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
   e.vec = a16(bias, 8) && a16(residual, ldr) && a16(gate, ldg) && a16(C, ldc) && a16(Cf, ldcf);

@@ -105,6 +105,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
     const int row = r0 + rr;
     if (row >= M) break;
     const float mu = mean[row], rs = rstd[row];
+    const uint32_t rowkey = thr ? smer_rowkey(seed, (uint32_t)row) : 0u;
     float xh[LN_MAXC][8], gd[LN_MAXC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -139,9 +140,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
         for (int i = 0; i < 8; ++i) o[i] = rs * (gd[c][i] - s1 - xh[c][i] * s2);
         Vec8<T>::store(dx + (long)row * lddx + ch * 8, o);
         if (dxd) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            o[i] = (thr == 0u || smer_keep(seed, thr, (uint32_t)row, (uint32_t)(ch * 8 + i))) ? o[i] * dscale : 0.f;
+          if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)(ch * 8), o);
           Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
         }
       }
@@ -194,7 +193,7 @@ __global__ void embed_fwd_kernel(int n_tok, int d, const int64_t* __restrict__ i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     float w = v[i];
-    if (thr) w = smer_keep(seed, thr, (uint32_t)t, (uint32_t)(c + i)) ? w * dscale : 0.f;
+    if (thr) w = smer_keep16(smer_rowkey(seed, (uint32_t)t), thr, (uint32_t)(c + i)) ? w * dscale : 0.f;
     o[i] = from_f32<T>(w);
   }
 }
@@ -236,7 +235,7 @@ __global__ __launch_bounds__(256) void embed_bwd_gather(
         if (i < ncol) {
           int col = lane + 64 * i;
           float g = s0 ? to_f32(dx0[(long)tl * ld0 + col]) : to_f32(dx1[(long)tl * ld1 + col]);
-          if (thr) g = smer_keep(sd, thr, (uint32_t)tl, (uint32_t)col) ? g * dsc : 0.f;
+          if (thr) g = smer_keep16(smer_rowkey(sd, (uint32_t)tl), thr, (uint32_t)col) ? g * dsc : 0.f;
           acc[i] += g;
         }
       }
@@ -302,8 +301,8 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   int nblk = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-  uint32_t thr = smer_drop_threshold(drop_p);
-  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  uint32_t thr = smer_drop_thr16(drop_p);
+  float ds = smer_drop_scale16(thr);
   float* part = params ? (float*)workspace : nullptr;
 #define LNB(T, F)                                                                              \
   hipLaunchKernelGGL((ln_bwd_kernel<T, F>), dim3(nblk), dim3(256), 0, s, M, N, dy, lddy,       \
@@ -332,8 +331,8 @@ extern "C" int smer_embed_fwd(int dtype, int n_tok, int d, const int64_t* ids,
   if (n_tok == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   long tot = (long)n_tok * (d / 4);
-  uint32_t thr = smer_drop_threshold(drop_p);
-  float ds = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  uint32_t thr = smer_drop_thr16(drop_p);
+  float ds = smer_drop_scale16(thr);
   if (dtype == SMER_BF16)
     hipLaunchKernelGGL(embed_fwd_kernel<bf16>, dim3((tot + 255) / 256), dim3(256), 0, s, n_tok, d,
                        ids, positions, L, table, pe, scale, thr, seed, ds, (bf16*)out, ldo);
@@ -364,8 +363,8 @@ extern "C" int smer_embed_bwd(int dtype, int V, int d, float scale, const int64_
   if (n == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   int nchunk = (n + EMB_CHUNK - 1) / EMB_CHUNK;
-  uint32_t t0 = smer_drop_threshold(p0), t1 = smer_drop_threshold(p1);
-  float ds0 = p0 > 0.f ? 1.f / (1.f - p0) : 1.f, ds1 = p1 > 0.f ? 1.f / (1.f - p1) : 1.f;
+  uint32_t t0 = smer_drop_thr16(p0), t1 = smer_drop_thr16(p1);
+  float ds0 = smer_drop_scale16(t0), ds1 = smer_drop_scale16(t1);
   dim3 grid(V, nchunk);
   if (dtype == SMER_BF16)
     hipLaunchKernelGGL(embed_bwd_gather<bf16>, grid, dim3(256), 0, s, V, d, ids0, (const bf16*)dx0,

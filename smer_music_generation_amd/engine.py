@@ -311,7 +311,7 @@ class Engine:
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1])
-            dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=1.0 / (1.0 - p_tr))
+            dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
             ops.linear_wgrad(dy3d, h, GL.l2_w)
             ops.colsum(dy3d, GL.l2_b)
             dx2 = ops.linear_dgrad(dh, L.l1_w, residual=dy3)
@@ -367,7 +367,7 @@ class Engine:
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
-            dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=1.0 / (1.0 - p_tr))
+            dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
             ops.linear_wgrad(dy2d, h, GL.l2_w)
             ops.colsum(dy2d, GL.l2_b)
             dx1 = ops.linear_dgrad(dh, L.l1_w, residual=dy2)

@@ -30,6 +30,15 @@ def _p(t):
     return t.data_ptr()
 
 
+def drop_scale(p):
+    """Survivor scale of every dropout site (csrc/common.h
+    smer_drop_scale16): 65536 / (65536 - round(p * 65536))."""
+    if p <= 0:
+        return 1.0
+    thr = min(65535, max(1, int(p * 65536.0 + 0.5)))
+    return 65536.0 / (65536.0 - thr)
+
+
 def _stream():
     return torch.cuda.current_stream().cuda_stream
 

@@ -109,7 +109,7 @@ def test_gemm_epilogue(dtype, M, N, K):
     C = torch.empty(M, N, device=dev, dtype=dtype)
     O.gemm(A, W, M=M, N=N, K=K, out=C, bias=bias, relu=True, residual=R, drop_p=p, seed=seed)
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    ref = R.float() + torch.where(keep, torch.relu(base + bias) / (1 - p), torch.zeros_like(base))
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < tol
     # gate (relu-backward) + fp32 accumulate
@@ -330,7 +330,7 @@ def test_layernorm(dtype, M, N):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     assert rel_err(dx, xf.grad) < tol
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    assert rel_err(dxd, torch.where(keep, xf.grad / (1 - p), torch.zeros_like(xf.grad))) < tol
+    assert rel_err(dxd, torch.where(keep, xf.grad * attn_scale(p), torch.zeros_like(xf.grad))) < tol
     assert rel_err(dg, gf.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
     assert rel_err(db, bf.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
 
@@ -350,7 +350,7 @@ def test_embedding(dtype):
     keep = torch.from_numpy(keep_mask(seed, p, B * L, d)).to(dev)
     pos = torch.arange(B * L, device=dev) % L
     ref = table[ids.view(-1)] * math.sqrt(d) + pe[pos]
-    ref = torch.where(keep, ref / (1 - p), torch.zeros_like(ref))
+    ref = torch.where(keep, ref * attn_scale(p), torch.zeros_like(ref))
     torch.cuda.synchronize()
     assert rel_err(out, ref) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
     ids2 = torch.randint(0, V, (2, 30), device=dev)
@@ -359,7 +359,7 @@ def test_embedding(dtype):
     dt = torch.zeros(V, d, device=dev)
     O.embed_bwd(dt, math.sqrt(d), [(ids.view(-1), dx0, p, seed), (ids2.view(-1), dx1, 0.0, 0)])
     ref = torch.zeros(V, d, device=dev)
-    g0 = torch.where(keep, dx0.float() / (1 - p), torch.zeros_like(dx0.float()))
+    g0 = torch.where(keep, dx0.float() * attn_scale(p), torch.zeros_like(dx0.float()))
     ref.index_add_(0, ids.view(-1), g0)
     ref.index_add_(0, ids2.view(-1), dx1.float())
     ref *= math.sqrt(d)
