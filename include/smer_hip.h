@@ -29,6 +29,9 @@
  *   smer_wce_*           the 7-12 weighted cross-entropy criteria fused into
  *                        one pass (train.py:555-642,726-780)
  *   smer_adam            torch.optim.Adam step (train.py:264,786)
+ *   smer_gemm_wgrad_bias nn.Linear weight AND bias gradients in one pass
+ *                        (autograd of transformer.py:389-469 / model.py:106
+ *                        linears, train.py:783)
  *   smer_colsum          bias gradients (autograd of nn.Linear bias)
  *   smer_cast            fp32 master -> bf16 working copies
  */
@@ -73,6 +76,18 @@ int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
               float drop_p, uint32_t drop_seed,
               void* C, long ldc, float* Cf, long ldcf, int accumulate,
               void* workspace, size_t ws_bytes, smer_stream_t stream);
+
+/* Weight + bias gradient of y = x W^T + b (bf16):
+ *   dW[M,N] (+)= dy^T x,  db[M] (+)= sum_k dy[k, :]
+ * dy: [K, M] row-major (K = tokens, ld lddy), x: [K, N] (ld ldx); dW fp32.
+ * The bias sum rides the GEMM as one extra MFMA against a ones fragment in
+ * the first column-tile's workgroups; with split-K both are reduced by the
+ * same deterministic pass.  workspace as smer_gemm (slabs + M floats per
+ * K slice).  fp32 returns SMER_ERR_UNSUPPORTED (use smer_gemm + smer_colsum). */
+int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long lddy,
+                         const void* x, long ldx, float* dW, long lddw, int accumulate,
+                         float* db, int db_accumulate, void* workspace, size_t ws_bytes,
+                         smer_stream_t stream);
 
 /* Flash attention over [B*L, *] token-row layouts (row = b*L + i), head h
  * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:

@@ -89,8 +89,11 @@ static inline float smer_drop_scale16(uint32_t thr16) {
 // (deterministic; two levels when nblk > 64, `scratch` of
 // smer_col_reduce_scratch(nblk, N) bytes).  Defined in train_ops.hip.
 size_t smer_col_reduce_scratch(int nblk, int N);
+// Columns >= nsplit of the reduced row go to out2[col - nsplit] (out2 may be
+// null: everything to out).
 void smer_col_reduce_launch(int nblk, int N, const float* part, long stride, long off, float* out,
-                            int accumulate, float scale, float* scratch, hipStream_t s);
+                            int accumulate, float scale, float* scratch, hipStream_t s,
+                            float* out2 = nullptr, int nsplit = 0);
 
 // Load 8 consecutive elements as floats (16-B vector when aligned & in range).
 template <typename T, bool VEC = true>

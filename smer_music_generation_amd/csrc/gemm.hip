@@ -31,6 +31,7 @@ struct GemmEpi {
   long ldcf;
   int accumulate;
   int vec;  // every operand 16-B aligned with row strides % 8 == 0
+  int rs_accumulate;  // fused row-sum output (bias gradient) accumulates
 };
 
 template <typename T>
@@ -176,7 +177,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
                                                            const bf16* __restrict__ A, long lda,
                                                            const bf16* __restrict__ B, long ldb,
                                                            GemmEpi e, int ksplit, int kchunk,
-                                                           float* __restrict__ slabs) {
+                                                           float* __restrict__ slabs,
+                                                           float* __restrict__ rowsum) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -208,6 +210,14 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // Fused bias gradient (weight-gradient GEMMs): the first column-tile's
+  // blocks also form sum_k A[m][k] with one extra MFMA against a ones
+  // fragment per 16 rows (the two wn waves split the 4 row fragments).
+  const bool rsum = rowsum != nullptr && tn == 0;
+  f32x4 accr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
 
   uint4 ra[4], rb[4];
   const int nk = (k_end - k_begin + GBK - 1) / GBK;
@@ -237,6 +247,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      if (rsum) {
+        accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
+        accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
+      }
     }
     if (more) {
       stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
@@ -245,6 +259,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
     __syncthreads();
   }
 
+  if (rsum && (lane & 15) == 0) {
+    // D[row 4g+r][any col] = row sum; partial per K slice, or the final sum
+    // (accumulated in place) when K is not split
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 64 + (2 * wn + j) * 16 + 4 * (lane >> 4) + r;
+        if (row < M) {
+          if (ksplit > 1) rowsum[(long)split * M + row] = accr[j][r];
+          else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + accr[j][r] * e.alpha;
+        }
+      }
+  }
   // Epilogue through LDS: each wave-half (wm) parks its 64x128 fp32 tile in
   // LDS, then all 256 threads walk it row-contiguously, 8 columns each, so
   // bias / residual / gate reads and C / Cf / slab writes are 16-B vectors
@@ -368,13 +396,22 @@ __global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int
   }
 }
 
-// Cf[m, n] (+)= alpha * sum_s slab[s][m][n]   (fixed order: deterministic)
+// Cf[m, n] (+)= alpha * sum_s slab[s][m][n]   (fixed order: deterministic);
+// threads past M*N/4 reduce the fused bias-gradient partials the same way.
 __global__ void splitk_reduce_kernel(int M, int N, int ksplit, const float* __restrict__ slabs,
                                      float alpha, float* __restrict__ Cf, long ldcf,
-                                     int accumulate) {
+                                     int accumulate, const float* __restrict__ rs_part,
+                                     float* __restrict__ rs_out, int rs_accumulate) {
   long idx = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   long MN = (long)M * N;
-  if (idx >= MN) return;
+  if (idx >= MN) {
+    const long m = ((long)blockIdx.x * blockDim.x + threadIdx.x) - MN / 4;
+    if (rs_out == nullptr || m >= M) return;
+    float t = 0.f;
+    for (int s = 0; s < ksplit; ++s) t += rs_part[(long)s * M + m];
+    rs_out[m] = (rs_accumulate ? rs_out[m] : 0.f) + alpha * t;
+    return;
+  }
   float4 a = *reinterpret_cast<const float4*>(slabs + idx);
   for (int s = 1; s < ksplit; ++s) {
     float4 b = *reinterpret_cast<const float4*>(slabs + (long)s * MN + idx);
@@ -455,15 +492,17 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   if (tiles >= 512 || K < 1024 || ((long)M * N) % 4 != 0) return 1;
   long s = (1024 + tiles - 1) / tiles;
   s = std::min<long>(s, K / 512);
-  s = std::min<long>(s, (long)(ws_bytes / ((size_t)M * N * sizeof(float))));
+  // slabs of M*N floats plus M floats of row-sum partials per K slice
+  s = std::min<long>(s, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
   s = std::max<long>(1, std::min<long>(s, 64));
   return (int)s;
 }
 
 template <bool AK, bool BKC>
 static void launch_bf16(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                        const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (AK && BKC && M <= 4 * SK_BM) {
+                        const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s,
+                        float* rowsum = nullptr) {
+  if (AK && BKC && M <= 4 * SK_BM && !rowsum) {
     hipLaunchKernelGGL(gemm_skinny_bf16_kernel, dim3((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM),
                        dim3(64 * SK_WAVES), 0, s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
     return;
@@ -475,13 +514,15 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     kchunk = ((K + split - 1) / split + GBK - 1) / GBK * GBK;
     split = (K + kchunk - 1) / kchunk;
   }
+  float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC>), dim3(tiles * split), dim3(256), 4 * TILE_BYTES,
                      s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
-                     (float*)ws);
+                     (float*)ws, split > 1 ? rs_part : rowsum);
   if (split > 1) {
-    long n4 = ((long)M * N) / 4;
+    long n4 = ((long)M * N) / 4 + (rowsum ? M : 0);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,
-                       (const float*)ws, e.alpha, e.Cf, e.ldcf, e.accumulate);
+                       (const float*)ws, e.alpha, e.Cf, e.ldcf, e.accumulate,
+                       (const float*)rs_part, rowsum, e.rs_accumulate);
   }
 }
 template <bool AK, bool BKC>
@@ -511,6 +552,7 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
   e.drop_thr = smer_drop_thr16(drop_p); e.seed = drop_seed;
   e.drop_scale = smer_drop_scale16(e.drop_thr);
   e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf; e.accumulate = accumulate;
+  e.rs_accumulate = 0;
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
   e.vec = a16(bias, 8) && a16(residual, ldr) && a16(gate, ldg) && a16(C, ldc) && a16(Cf, ldcf);
   hipStream_t s = (hipStream_t)stream;
@@ -537,5 +579,27 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm: dtype");
   }
   SMER_CHECK_LAUNCH("smer_gemm");
+  return SMER_OK;
+}
+
+extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long lddy,
+                                    const void* x, long ldx, float* dW, long lddw, int accumulate,
+                                    float* db, int db_accumulate, void* workspace,
+                                    size_t ws_bytes, smer_stream_t stream) {
+  SMER_REQUIRE(dtype == SMER_BF16, "smer_gemm_wgrad_bias: bf16 only (fp32: smer_gemm + smer_colsum)");
+  SMER_REQUIRE(M > 0 && N > 0 && K > 0, "smer_gemm_wgrad_bias: bad sizes");
+  SMER_REQUIRE(dy && x && dW && db, "smer_gemm_wgrad_bias: null pointer");
+  SMER_REQUIRE(lddy % 8 == 0 && ldx % 8 == 0 && lddy >= (long)((M + 7) / 8) * 8 &&
+                   ldx >= (long)((N + 7) / 8) * 8,
+               "smer_gemm_wgrad_bias: dy / x row strides");
+  SMER_REQUIRE(aligned16(dy) && aligned16(x) && (!workspace || aligned16(workspace)),
+               "smer_gemm_wgrad_bias: 16-B alignment");
+  GemmEpi e{};
+  e.alpha = 1.f; e.drop_scale = 1.f;
+  e.Cf = dW; e.ldcf = lddw; e.accumulate = accumulate; e.rs_accumulate = db_accumulate;
+  auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
+  e.vec = a16(dW, lddw);
+  launch_bf16<false, false>(M, N, K, dy, lddy, x, ldx, e, workspace, ws_bytes, (hipStream_t)stream, db);
+  SMER_CHECK_LAUNCH("smer_gemm_wgrad_bias");
   return SMER_OK;
 }

@@ -284,7 +284,7 @@ extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long l
 
 extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
   size_t nblk = (size_t)(M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
-  return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, N);
+  return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, 2 * N);
 }
 
 extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
@@ -312,10 +312,13 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   else if (dtype == SMER_F32) { LNB(float, false); }
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
-  if (dgamma)
+  if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
+    smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
+                           part + (size_t)nblk * 2 * N, s, dbeta, N);
+  else if (dgamma)
     smer_col_reduce_launch(nblk, N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s);
-  if (dbeta)
+  else if (dbeta)
     smer_col_reduce_launch(nblk, N, part, (long)2 * N, (long)N, dbeta, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s);
   SMER_CHECK_LAUNCH("smer_layernorm_bwd");

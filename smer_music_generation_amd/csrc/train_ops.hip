@@ -138,11 +138,13 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(int M, int N, const T*
 }
 
 // Workgroup (x = 64-column tile, y = chunk of `chunk` partial rows) writes
-// out[y * ostride + col]; rows summed in a fixed order (deterministic).
+// out[y * ostride + col] (columns >= nsplit go to out2[col - nsplit]); rows
+// summed in a fixed order (deterministic).
 __global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const float* __restrict__ part,
                                                        long stride, long off, float* __restrict__ out,
                                                        long ostride, int chunk, int accumulate,
-                                                       float scale) {
+                                                       float scale, float* __restrict__ out2,
+                                                       int nsplit) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
@@ -163,7 +165,8 @@ __global__ void __launch_bounds__(256) smer_col_reduce(int nblk, int N, const fl
   __syncthreads();
   if (g == 0 && col < N) {
     float a = ((red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl])) * scale;
-    float* o = out + (long)blockIdx.y * ostride + col;
+    float* o = col < nsplit ? out + (long)blockIdx.y * ostride + col
+                            : out2 + (long)blockIdx.y * ostride + (col - nsplit);
     *o = accumulate ? *o + a : a;
   }
 }
@@ -173,17 +176,20 @@ size_t smer_col_reduce_scratch(int nblk, int N) {
 }
 
 void smer_col_reduce_launch(int nblk, int N, const float* part, long stride, long off, float* out,
-                            int accumulate, float scale, float* scratch, hipStream_t s) {
+                            int accumulate, float scale, float* scratch, hipStream_t s,
+                            float* out2, int nsplit) {
   dim3 gx((N + 63) / 64);
+  if (!out2) nsplit = N;
   if (nblk > 64) {
     int g = (nblk + 63) / 64;
     hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, g), dim3(256), 0, s, nblk, N, part, stride,
-                       off, scratch, (long)N, 64, 0, 1.f);
+                       off, scratch, (long)N, 64, 0, 1.f, (float*)nullptr, N);
     hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, 1), dim3(256), 0, s, g, N,
-                       (const float*)scratch, (long)N, 0L, out, 0L, g, accumulate, scale);
+                       (const float*)scratch, (long)N, 0L, out, 0L, g, accumulate, scale, out2,
+                       nsplit);
   } else {
     hipLaunchKernelGGL(smer_col_reduce, dim3(gx.x, 1), dim3(256), 0, s, nblk, N, part, stride,
-                       off, out, 0L, nblk, accumulate, scale);
+                       off, out, 0L, nblk, accumulate, scale, out2, nsplit);
   }
 }
 

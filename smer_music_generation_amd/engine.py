@@ -292,8 +292,7 @@ class Engine:
 
         # vocab head
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
-        ops.linear_wgrad(dlog_pad, ctx.dec_out, G.fc_w, M=V)
-        ops.colsum(dlog_pad, G.fc_b, N=V)
+        ops.linear_wgrad(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         # final decoder norm
         y_last, mo, ro = ctx.dec_last
         dy = torch.empty_like(y_last)
@@ -312,46 +311,39 @@ class Engine:
             ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1])
             dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
-            ops.linear_wgrad(dy3d, h, GL.l2_w)
-            ops.colsum(dy3d, GL.l2_b)
+            ops.linear_wgrad(dy3d, h, GL.l2_w, db=GL.l2_b)
             dx2 = ops.linear_dgrad(dh, L.l1_w, residual=dy3)
-            ops.linear_wgrad(dh, x2, GL.l1_w)
-            ops.colsum(dh, GL.l1_b)
+            ops.linear_wgrad(dh, x2, GL.l1_w, db=GL.l1_b)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx2, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
             doc = ops.linear_dgrad(dy2d, L.ca_ow)
-            ops.linear_wgrad(dy2d, oc, GL.ca_ow)
-            ops.colsum(dy2d, GL.ca_ob)
+            ops.linear_wgrad(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = torch.empty(Ms, 2 * d, dtype=dt, device=dev)
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)))
             dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
-            ops.linear_wgrad(dqc, x1, GL.cq_w)
-            ops.colsum(dqc, GL.cq_b)
+            ops.linear_wgrad(dqc, x1, GL.cq_w, db=GL.cq_b)
             ops.linear_dgrad(dkvc, L.ckv_w, out_f32=dmem, accumulate=True)
-            ops.linear_wgrad(dkvc, ctx.mem, GL.ckv_w)
-            ops.colsum(dkvc, GL.ckv_b)
+            ops.linear_wgrad(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
             # self-attention block
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
             do = ops.linear_dgrad(dy1d, L.sa_ow)
-            ops.linear_wgrad(dy1d, o, GL.sa_ow)
-            ops.colsum(dy1d, GL.sa_ob)
+            ops.linear_wgrad(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
                          seed=sd(_site("dec", i, 0)))
             dy = ops.linear_dgrad(dqkv, L.sa_w, residual=dy1)
-            ops.linear_wgrad(dqkv, y_in, GL.sa_w)
-            ops.colsum(dqkv, GL.sa_b)
+            ops.linear_wgrad(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             if hook:
                 hook("dec%d" % i)
         d_tgt = dy
@@ -368,26 +360,22 @@ class Engine:
             ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
             dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
-            ops.linear_wgrad(dy2d, h, GL.l2_w)
-            ops.colsum(dy2d, GL.l2_b)
+            ops.linear_wgrad(dy2d, h, GL.l2_w, db=GL.l2_b)
             dx1 = ops.linear_dgrad(dh, L.l1_w, residual=dy2)
-            ops.linear_wgrad(dh, x1, GL.l1_w)
-            ops.colsum(dh, GL.l1_b)
+            ops.linear_wgrad(dh, x1, GL.l1_w, db=GL.l1_b)
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
             do = ops.linear_dgrad(dy1d, L.out_w)
-            ops.linear_wgrad(dy1d, o, GL.out_w)
-            ops.colsum(dy1d, GL.out_b)
+            ops.linear_wgrad(dy1d, o, GL.out_w, db=GL.out_b)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
                          seed=sd(_site("enc", i, 0)))
             dx = ops.linear_dgrad(dqkv, L.in_w, residual=dy1)
-            ops.linear_wgrad(dqkv, x_in, GL.in_w)
-            ops.colsum(dqkv, GL.in_b)
+            ops.linear_wgrad(dqkv, x_in, GL.in_w, db=GL.in_b)
             if hook:
                 hook("enc%d" % i)
         # shared embedding (model.py:76): both streams scatter into one table

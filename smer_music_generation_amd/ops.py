@@ -138,12 +138,29 @@ def linear_dgrad(dy, w, *, K=None, out=None, residual=None, gate=None, gate_scal
     return out if out is not None else out_f32
 
 
-def linear_wgrad(dy, x, dw, *, M=None, accumulate=True):
-    """dw (+)= dy^T @ x: dy [T, M_out(ld)], x [T, K_in] -> dw fp32 [M_out, K_in]."""
+def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None):
+    """dw (+)= dy^T @ x: dy [T, M_out(ld)], x [T, K_in] -> dw fp32 [M_out, K_in];
+    db (+)= column sums of dy when given (bf16: fused into the GEMM)."""
     T = dy.shape[0]
     Mo = M if M is not None else dy.shape[1]
+    if db is not None and dy.dtype == torch.bfloat16:
+        ws = splitk_workspace(dy.device)
+        timer = GEMM_TIMER
+        if timer is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        call("smer_gemm_wgrad_bias", BF16, Mo, x.shape[1], T, _p(dy), _ld(dy), _p(x), _ld(x),
+             _p(dw), _ld(dw), int(accumulate), _p(db), int(accumulate), _p(ws), ws.numel(),
+             _stream())
+        if timer is not None:
+            ev1.record()
+            timer.records.append((ev0, ev1, 2.0 * Mo * x.shape[1] * T))
+        return
     gemm(dy, x, M=Mo, N=x.shape[1], K=T, a_kcontig=False, b_kcontig=False, out_f32=dw,
          accumulate=accumulate, dtype=dy.dtype)
+    if db is not None:
+        colsum(dy, db, N=Mo, accumulate=accumulate)
 
 
 # ---------------------------------------------------------------------------
