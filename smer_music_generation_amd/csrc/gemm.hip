@@ -12,6 +12,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 struct GemmEpi {
   const float* bias;
@@ -152,6 +153,36 @@ __device__ __forceinline__ void stage_store(const uint4 (&r)[4], char* buf, int 
   }
 }
 
+// LDS-DMA staging (global_load_lds_dwordx4): each wave instruction writes
+// 1 KiB of the LDS image lane-linearly, so the XOR swizzle of the image is
+// applied to the per-lane SOURCE address instead (lane i fills physical
+// chunk i and fetches the logical chunk that belongs there).  No VGPR round
+// trip and no ds_write.  Rows past `rows` are clamped (their products only
+// reach discarded outputs); the caller guarantees the K range is full.
+template <bool KC>
+__device__ __forceinline__ void stage_glds(char* buf, const bf16* P, long ld, int rows,
+                                           int r0, int k0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int chunk = wave * 4 + c;  // 16 x 1 KiB per 16 KiB operand tile
+    const bf16* src;
+    if (KC) {
+      const int row = chunk * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (row & 7);
+      src = P + (long)min(r0 + row, rows - 1) * ld + k0 + lc * 8;
+    } else {
+      const int k = chunk * 4 + (lane >> 4);
+      const int lc = (lane & 15) ^ (2 * (int)col_swz(k));
+      const int col = min(r0 + lc * 8, ((rows + 7) & ~7) - 8);
+      src = P + (long)(k0 + k) * ld + col;
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
+  }
+}
+
 // Fragment (16 rows starting at rbase, k-step s) for lane l.
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int lane) {
@@ -172,7 +203,7 @@ __device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int la
 }
 }  // namespace
 
-template <bool AK, bool BKC>
+template <bool AK, bool BKC, bool GL>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
                                                            const bf16* __restrict__ A, long lda,
                                                            const bf16* __restrict__ B, long ldb,
@@ -183,141 +214,179 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = (M + GBM - 1) / GBM, nbn = (N + GBN - 1) / GBN;
-  const int nwg = nbm * nbn * ksplit;
-  // Bijective XCD remap (blocks b and b+8 share an XCD): each XCD gets a
-  // contiguous run of work items; the K slices of one tile are adjacent
-  // (same XCD), tiles are walked in GM-row groups for L2 reuse.
-  const int braw = blockIdx.x;
-  const int xcd = braw & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (braw >> 3);
-  // tile-major within a K slice: blocks that run together on one XCD share
-  // the slice's A and B panels in that XCD's L2
   const int ntiles = nbm * nbn;
-  const int split = lin / ntiles;
-  const int wgid = lin % ntiles;
+  const int nwg = ntiles * ksplit;
+  // Persistent, XCD-aware work list: XCD x (blocks b with b % 8 == x) owns a
+  // contiguous run of work items and its blocks stride through it; the K
+  // slices of one tile are adjacent, tiles are walked in GM-row groups, so
+  // blocks running together on one XCD share A / B panels in its L2.  With
+  // a grid of exactly nwg blocks every block takes one item (bijective).
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
   constexpr int GM = 8;
-  const int grp = wgid / (GM * nbn);
-  const int first_m = grp * GM;
-  const int gsz = min(nbm - first_m, GM);
-  const int within = wgid % (GM * nbn);
-  const int tm = first_m + within % gsz, tn = within / gsz;
-  const int m0 = tm * GBM, n0 = tn * GBN;
-  const int k_begin = split * kchunk;
-  const int k_end = min(K, k_begin + kchunk);
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Fused bias gradient (weight-gradient GEMMs): the first column-tile's
-  // blocks also form sum_k A[m][k] with one extra MFMA against a ones
-  // fragment per 16 rows (the two wn waves split the 4 row fragments).
-  const bool rsum = rowsum != nullptr && tn == 0;
-  f32x4 accr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  struct Item { int split, tm, tn, m0, n0, k_begin, k_end; };
+  auto decode = [&](int lin) {
+    Item it;
+    it.split = lin / ntiles;
+    const int wgid = lin % ntiles;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    it.tm = first_m + within % gsz;
+    it.tn = within / gsz;
+    it.m0 = it.tm * GBM;
+    it.n0 = it.tn * GBN;
+    it.k_begin = it.split * kchunk;
+    it.k_end = min(K, it.k_begin + kchunk);
+    return it;
+  };
   bf16x8 ones;
 #pragma unroll
   for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
-
   uint4 ra[4], rb[4];
-  const int nk = (k_end - k_begin + GBK - 1) / GBK;
-  stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin, tid);
-  stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin, tid);
-  stage_store<AK>(ra, smem, tid);
-  stage_store<BKC>(rb, smem + TILE_BYTES, tid);
-  __syncthreads();
+  bool prefetched = false;
 
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin + (kt + 1) * GBK, tid);
-      stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin + (kt + 1) * GBK, tid);
-    }
-    const char* a_s = smem + cur * 2 * TILE_BYTES;
-    const char* b_s = a_s + TILE_BYTES;
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const Item it = decode(xstart + jj);
+    const int m0 = it.m0, n0 = it.n0, k_begin = it.k_begin, k_end = it.k_end;
+
+    f32x4 acc[4][4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[4], bfr[4];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(a_s, wm * 64 + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      if (rsum) {
-        accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
-        accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Fused bias gradient (weight-gradient GEMMs): the first column-tile's
+    // blocks also form sum_k A[m][k] with one extra MFMA against a ones
+    // fragment per 16 rows (the two wn waves split the 4 row fragments).
+    const bool rsum = rowsum != nullptr && it.tn == 0;
+    f32x4 accr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+
+    const int nk = (k_end - k_begin + GBK - 1) / GBK;
+    if constexpr (GL) {
+      stage_glds<AK>(smem, A, lda, M, m0, k_begin, tid);
+      stage_glds<BKC>(smem + TILE_BYTES, B, ldb, N, n0, k_begin, tid);
+    } else {
+      if (!prefetched) {
+        stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin, tid);
+        stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin, tid);
       }
-    }
-    if (more) {
-      stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
-      stage_store<BKC>(rb, smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES, tid);
+      stage_store<AK>(ra, smem, tid);
+      stage_store<BKC>(rb, smem + TILE_BYTES, tid);
     }
     __syncthreads();
-  }
 
-  if (rsum && (lane & 15) == 0) {
-    // D[row 4g+r][any col] = row sum; partial per K slice, or the final sum
-    // (accumulated in place) when K is not split
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if constexpr (GL) {
+        if (more) {
+          char* nb = smem + (cur ^ 1) * 2 * TILE_BYTES;
+          stage_glds<AK>(nb, A, lda, M, m0, k_begin + (kt + 1) * GBK, tid);
+          stage_glds<BKC>(nb + TILE_BYTES, B, ldb, N, n0, k_begin + (kt + 1) * GBK, tid);
+        }
+      } else if (more) {
+        stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin + (kt + 1) * GBK, tid);
+        stage_load<BKC>(rb, B, ldb, N, k_end, n0, k_begin + (kt + 1) * GBK, tid);
+      }
+      const char* a_s = smem + cur * 2 * TILE_BYTES;
+      const char* b_s = a_s + TILE_BYTES;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + (2 * wn + j) * 16 + 4 * (lane >> 4) + r;
-        if (row < M) {
-          if (ksplit > 1) rowsum[(long)split * M + row] = accr[j][r];
-          else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + accr[j][r] * e.alpha;
+        for (int i = 0; i < 4; ++i) af[i] = frag<AK>(a_s, wm * 64 + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        if (rsum) {
+          accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
+          accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
         }
       }
-  }
-  // Epilogue through LDS: each wave-half (wm) parks its 64x128 fp32 tile in
-  // LDS, then all 256 threads walk it row-contiguously, 8 columns each, so
-  // bias / residual / gate reads and C / Cf / slab writes are 16-B vectors
-  // and 16 consecutive lanes cover one 256-B (bf16) row segment.
-  const int g = lane >> 4, c16 = lane & 15;
-  constexpr int EP_LD = GBN + 4;
-  float* ep = reinterpret_cast<float*>(smem);
-  float* slab = ksplit > 1 ? slabs + (long)split * M * N : nullptr;
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (wm == half) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ep[(i * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+      if (!GL && more) {
+        stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
+        stage_store<BKC>(rb, smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES, tid);
+      }
+      __syncthreads();
     }
-    __syncthreads();
+
+    // prefetch the next item's first K stage: its load latency hides behind
+    // this item's epilogue (register staging only: the LDS-DMA stage would
+    // land under the epilogue's LDS tile)
+    prefetched = !GL && jj + pstride < xcount;
+    if (prefetched) {
+      const Item nx = decode(xstart + jj + pstride);
+      stage_load<AK>(ra, A, lda, M, nx.k_end, nx.m0, nx.k_begin, tid);
+      stage_load<BKC>(rb, B, ldb, N, nx.k_end, nx.n0, nx.k_begin, tid);
+    }
+
+    if (rsum && (lane & 15) == 0) {
+      // D[row 4g+r][any col] = row sum; partial per K slice, or the final
+      // sum (accumulated in place) when K is not split
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int item = tid + 256 * c;
-      const int row = item >> 4, ch = item & 15;
-      const int grow = m0 + half * 64 + row, gcol = n0 + ch * 8;
-      if (grow < M && gcol < N) {
-        float v[8];
-        const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
-        const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        if (slab) {
-          const int valid = min(8, N - gcol);
-          float* dst = slab + (long)grow * N + gcol;
-          if (valid == 8 && (N & 3) == 0) {
-            *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
-          } else {
-            for (int k = 0; k < valid; ++k) dst[k] = v[k];
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 64 + (2 * wn + j) * 16 + 4 * (lane >> 4) + r;
+          if (row < M) {
+            if (ksplit > 1) rowsum[(long)it.split * M + row] = accr[j][r];
+            else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + accr[j][r] * e.alpha;
           }
-        } else {
-          epi_apply8(e, M, N, grow, gcol, v);
+        }
+    }
+    // Epilogue through LDS: each wave-half (wm) parks its 64x128 fp32 tile in
+    // LDS, then all 256 threads walk it row-contiguously, 8 columns each, so
+    // bias / residual / gate reads and C / Cf / slab writes are 16-B vectors
+    // and 16 consecutive lanes cover one 256-B (bf16) row segment.
+    const int g = lane >> 4, c16 = lane & 15;
+    constexpr int EP_LD = GBN + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+    float* slab = ksplit > 1 ? slabs + (long)it.split * M * N : nullptr;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wm == half) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[(i * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int item = tid + 256 * c;
+        const int row = item >> 4, ch = item & 15;
+        const int grow = m0 + half * 64 + row, gcol = n0 + ch * 8;
+        if (grow < M && gcol < N) {
+          float v[8];
+          const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+          const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          if (slab) {
+            const int valid = min(8, N - gcol);
+            float* dst = slab + (long)grow * N + gcol;
+            if (valid == 8 && (N & 3) == 0) {
+              *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+              *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+              for (int k = 0; k < valid; ++k) dst[k] = v[k];
+            }
+          } else {
+            epi_apply8(e, M, N, grow, gcol, v);
+          }
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -485,6 +554,29 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K,
 // Split-K (deterministic slabs) for a pure Cf (+)= A.B^T epilogue with few
 // output tiles and a long K, i.e. the weight gradients (K = tokens): without
 // it a [512 x 1536] wgrad occupies 48 of 256 CUs.
+// SMER_GEMM_GLDS=0 forces register staging (A/B comparisons, tests).
+static bool smer_gemm_glds_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_GEMM_GLDS");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static int smer_num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -515,7 +607,14 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     split = (K + kchunk - 1) / kchunk;
   }
   float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
-  hipLaunchKernelGGL((gemm_bf16_kernel<AK, BKC>), dim3(tiles * split), dim3(256), 4 * TILE_BYTES,
+  // persistent grid: two resident workgroups per CU (LDS 64 KiB, <= 256 VGPRs)
+  const long nwg = (long)tiles * split;
+  const long resident = 2L * smer_num_cus();
+  const int grid = nwg > resident ? (int)(resident & ~7L) : (int)nwg;
+  // LDS-DMA staging needs whole 64-deep K steps in every slice
+  const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled();
+  auto kern = gl ? gemm_bf16_kernel<AK, BKC, true> : gemm_bf16_kernel<AK, BKC, false>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 4 * TILE_BYTES,
                      s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
                      (float*)ws, split > 1 ? rs_part : rowsum);
   if (split > 1) {

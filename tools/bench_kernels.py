@@ -61,8 +61,17 @@ def bench_gemm():
                                         out_f32=C, accumulate=True, dtype=bf))
             t2 = t
         fl = 2.0 * M * N * K
+        # vendor library reference point (torch -> hipBLASLt), same shapes / layouts
+        if kind == "nt":
+            tt = timeit(lambda: torch.mm(A, B.t(), out=C))
+        elif kind == "nn":
+            tt = timeit(lambda: torch.mm(A, B, out=C))
+        else:
+            Cb = torch.empty(M, N, device=dev, dtype=bf)
+            tt = timeit(lambda: torch.mm(A.t(), B, out=Cb))
         print("%-16s %s M=%6d N=%5d K=%6d  %8.1f us %7.1f TF   (epilogue: %8.1f us %7.1f TF)"
-              % (name, kind, M, N, K, t, fl / t / 1e6, t2, fl / t2 / 1e6))
+              "  [torch/hipBLASLt %7.1f TF]"
+              % (name, kind, M, N, K, t, fl / t / 1e6, t2, fl / t2 / 1e6, fl / tt / 1e6))
 
 
 def bench_attn():
