@@ -582,8 +582,11 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   if (!cf_only) return 1;
   long tiles = (long)((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   if (tiles >= 512 || K < 1024 || ((long)M * N) % 4 != 0) return 1;
-  long s = (1024 + tiles - 1) / tiles;
-  s = std::min<long>(s, K / 512);
+  // ~2 resident workgroups per CU, K slices >= 1024 deep: more slices only
+  // add slab traffic (split * M * N * 8 bytes through HBM)
+  // (floor: a partial second wave of workgroups costs a whole slice time)
+  long s = (2L * smer_num_cus()) / tiles;
+  s = std::min<long>(s, K / 1024);
   // slabs of M*N floats plus M floats of row-sum partials per K slice
   s = std::min<long>(s, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
   s = std::max<long>(1, std::min<long>(s, 64));
