@@ -96,14 +96,21 @@ int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long ld
 int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D,
                   const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                   void* o, long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
-                  float drop_p, uint32_t seed, smer_stream_t stream);
+                  float drop_p, uint32_t seed, void* drop_mask, smer_stream_t stream);
+/* drop_mask (nullable, 16-B aligned, smer_attn_drop_mask_bytes): with
+ * drop_p > 0 the bf16 forward also stores its keep bits (1 bit per
+ * (query, key), as four 64-bit wave ballots per 16x16 block) so that
+ * smer_attn_bwd reads them instead of re-hashing; the mask is the same
+ * either way. */
+size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk);
 size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int Lk);
 int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D,
                   const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                   const void* o, long ldo, const void* dout, long lddo, const float* lse,
                   const uint8_t* kpm, int causal, float scale, float drop_p, uint32_t seed,
                   void* dq, long lddq, void* dk, long lddk, void* dv, long lddv,
-                  void* workspace, size_t ws_bytes, smer_stream_t stream);
+                  void* workspace, size_t ws_bytes, const void* drop_mask,
+                  smer_stream_t stream);
 /* out fp32 [B, Lq, Lk] = mean over heads of the attention probabilities. */
 int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
                       const void* q, long ldq, const void* k, long ldk, const float* lse,

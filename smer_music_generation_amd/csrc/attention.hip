@@ -102,7 +102,9 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
                                                      float* __restrict__ lse,
                                                      const uint8_t* __restrict__ kpm, int causal,
                                                      float scale, uint32_t drop_thr, uint32_t seed,
-                                                     float drop_scale) {
+                                                     float drop_scale,
+                                                     uint64_t* __restrict__ drop_mask) {
+  // drop_mask: see smer_attn_drop_mask_bytes (16-bit words, one per lane)
   using C = AttnCfg<D>;
   constexpr int QB = 64 * QG;  // queries per block
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
@@ -116,6 +118,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
   const int bh = BY, b = bh / H, h = bh % H;
   const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
+  const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
 
   bf16x8 qf[QG][C::NS];
 #pragma unroll
@@ -223,16 +226,32 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
           l_run[gq] += p[mt][r];
         }
       if (DROP) {
-        // keys mt*16+4g+{0,1} and {2,3} share one hash
+        // keys mt*16+4g+{0,1} and {2,3} share one hash; the keep bits are
+        // also published as the 16x16 sub-block's four ballots (see
+        // smer_drop_mask_bytes) so the backward reads instead of re-hashing
         const uint32_t pb = (uint32_t)(t * (KVB / 2) + 2 * g);
+        uint32_t mword = 0u;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < 4; ++mt) {
+          bool kp[4];
 #pragma unroll
           for (int rp = 0; rp < 2; ++rp) {
             const uint32_t hb = smer_pair_bits(rowkey[gq], pb + mt * 8 + rp);
-            p[mt][2 * rp] = (hb & 0xFFFFu) >= drop_thr ? p[mt][2 * rp] * drop_scale : 0.f;
-            p[mt][2 * rp + 1] = (hb >> 16) >= drop_thr ? p[mt][2 * rp + 1] * drop_scale : 0.f;
+            kp[2 * rp] = (hb & 0xFFFFu) >= drop_thr;
+            kp[2 * rp + 1] = (hb >> 16) >= drop_thr;
           }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[mt][r] = kp[r] ? p[mt][r] * drop_scale : 0.f;
+            mword |= (uint32_t)kp[r] << (mt * 4 + r);
+          }
+        }
+        // this lane's 16 keep bits of (query c16 of group gq, key tile t):
+        // word [bh][q16][t][lane], bit 4mt + r = key t*64 + 16mt + 4g + r
+        const int q16 = (q0w + gq * 16) >> 4;
+        if (drop_mask && q16 < nq16)
+          reinterpret_cast<uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane] =
+              (uint16_t)mword;
       }
       m_run[gq] = m_new;
       pf[gq][0] = pack_p(p, 0);
@@ -276,56 +295,72 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
 // ---------------------------------------------------------------------------
 // bf16 backward: dK / dV
 // ---------------------------------------------------------------------------
-template <int D, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
+// KG key groups of 16 per wave (block = 64*KG keys): the Q / dO fragments
+// read from LDS per query tile feed KG groups.
+template <int D, bool DROP, int KG, bool MSK = false>
+__global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
     const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
     uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dk, long lddk,
-    bf16* __restrict__ dv, long lddv) {
+    bf16* __restrict__ dv, long lddv, const uint64_t* __restrict__ drop_mask) {
   using C = AttnCfg<D>;
+  constexpr int KB = 64 * KG;  // keys per block
+  const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   // per query of the staged tile: lse (log2 units; +inf past Lq so P = 0),
   // delta, and the dropout row key
   __shared__ __attribute__((aligned(16))) float s_lse[2][KVB];
   __shared__ __attribute__((aligned(16))) float s_del[2][KVB];
   __shared__ __attribute__((aligned(16))) uint32_t s_rk[2][KVB];
+  // forward's keep words of the staged query tile x this block's key tiles:
+  // [query 16-block][key tile][64 lanes] (16 bits each)
+  __shared__ __attribute__((aligned(16))) uint16_t s_msk[2][4][KG][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
   xcd_block2d(BX, BY);
   const int bh = BY, b = bh / H, h = bh % H;
-  const int kj = BX * 64 + wave * 16 + c16;
-  // padded keys get no gradient: their dK / dV rows are written as zeros
-  const bool kvalid = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
+  const int k0w = BX * KB + wave * 16 * KG;  // first key of this wave
   const float c = scale * LOG2E_F;
 
-  bf16x8 kf[C::NS], vf[C::NS];
-  {
+  bf16x8 kf[KG][C::NS], vf[KG][C::NS];
+  bool kvalid[KG];
+#pragma unroll
+  for (int gk = 0; gk < KG; ++gk) {
+    const int kj = k0w + gk * 16 + c16;
+    // padded keys get no gradient: their dK / dV rows are written as zeros
+    kvalid[gk] = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
     long row = (long)(b * Lk + min(kj, Lk - 1));
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(k + row * ldk + h * D + s * 32 + 8 * g);
-      vf[s] = *reinterpret_cast<const bf16x8*>(v + row * ldv + h * D + s * 32 + 8 * g);
+      kf[gk][s] = *reinterpret_cast<const bf16x8*>(k + row * ldk + h * D + s * 32 + 8 * g);
+      vf[gk][s] = *reinterpret_cast<const bf16x8*>(v + row * ldv + h * D + s * 32 + 8 * g);
     }
   }
   const bf16* qb = q + (long)b * Lq * ldq + h * D;
   const bf16* ob = dout + (long)b * Lq * lddo + h * D;
   const float* lb = lse + (long)bh * Lq;
   const float* db = delta + (long)bh * Lq;
-  const uint32_t kpair = (uint32_t)kj >> 1;
-  const bool khi = kj & 1;
 
   const int n_qt = (Lq + KVB - 1) / KVB;
-  const int t0 = causal ? min(n_qt, (BX * 64) / KVB) : 0;
-  f32x4 adk[C::NDT], adv[C::NDT];
+  const int t0 = causal ? min(n_qt, (BX * KB) / KVB) : 0;
+  f32x4 adk[KG][C::NDT], adv[KG][C::NDT];
 #pragma unroll
-  for (int i = 0; i < C::NDT; ++i) { adk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; adv[i] = adk[i]; }
+  for (int gk = 0; gk < KG; ++gk)
+#pragma unroll
+    for (int i = 0; i < C::NDT; ++i) {
+      adk[gk][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      adv[gk][i] = adk[gk][i];
+    }
 
   uint4 rq[C::CPT], ro[C::CPT];
   float rl = 0.f, rd = 0.f;
   uint32_t rr = 0u;
+  uint4 rm = make_uint4(0, 0, 0, 0);
+  constexpr int MCH = KG * 128 / 16;  // 16-B chunks per query 16-block row
+  constexpr bool use_mask = DROP && MSK;
   auto load = [&](int t) {
     tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
     tile_load<D>(ro, ob, lddo, t * KVB, Lq, tid);
@@ -333,7 +368,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
       int qq = t * KVB + tid;
       rl = qq < Lq ? lb[qq] * LOG2E_F : INFINITY;
       rd = qq < Lq ? db[qq] : 0.f;
-      if (DROP) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
+      if (DROP && !MSK) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
+    }
+    if (use_mask && tid < 4 * MCH) {
+      const int qr = tid / MCH, ch = tid % MCH;
+      const int q16 = t * 4 + qr, kt = BX * KG + ch / 8;
+      rm = (q16 < nq16 && kt < nkt)
+               ? reinterpret_cast<const uint4*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + kt) * 8 + (ch & 7)]
+               : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&](int buf) {
@@ -342,8 +384,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     if (tid < KVB) {
       s_lse[buf][tid] = rl;
       s_del[buf][tid] = rd;
-      if (DROP) s_rk[buf][tid] = rr;
+      if (DROP && !MSK) s_rk[buf][tid] = rr;
     }
+    if (use_mask && tid < 4 * MCH)
+      reinterpret_cast<uint4*>(&s_msk[buf][0][0][0])[tid] = rm;
   };
   if (t0 < n_qt) { load(t0); store(0); }
   __syncthreads();
@@ -353,98 +397,155 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_bf16(
     if (more) load(t + 1);
     const char* Qs = sm[cur][0];
     const char* Os = sm[cur][1];
-    const bool diag = causal && t * KVB < BX * 64 + 64;
-    float pd[4][4], ds[4][4];
+    // some key of this wave is later than some query of the tile
+    const bool diag = causal && t * KVB < k0w + 16 * KG;
+    bf16x8 pf[KG][2], sf[KG][2];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
+    for (int gk = 0; gk < KG; ++gk) {
+      const int kj = k0w + gk * 16 + c16;
+      const uint32_t kpair = (uint32_t)kj >> 1;
+      const bool khi = kj & 1;
+      float pd[4][4], ds[4][4];
+      const int k16 = (k0w + gk * 16) >> 4;
 #pragma unroll
-      for (int s = 0; s < C::NS; ++s) {
-        sacc = mfma16(row_frag<D>(Qs, mt * 16, s, lane), kf[s], sacc);
-        dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[s], dpacc);
-      }
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
+      for (int mt = 0; mt < 4; ++mt) {
+        f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = fast_exp2(fmaf(sacc[r], c, -l4[r]));
-        if (diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
-        float dpv = dpacc[r];
-        float pdv = pv;
-        if (DROP) {
-          const uint32_t hb = smer_pair_bits(s_rk[cur][mt * 16 + 4 * g + r], kpair);
-          const bool keep = (khi ? (hb >> 16) : (hb & 0xFFFFu)) >= drop_thr;
-          pdv = keep ? pv * drop_scale : 0.f;
-          dpv = keep ? dpv * drop_scale : 0.f;
+        for (int s = 0; s < C::NS; ++s) {
+          sacc = mfma16(row_frag<D>(Qs, mt * 16, s, lane), kf[gk][s], sacc);
+          dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[gk][s], dpacc);
         }
-        pd[mt][r] = pdv;
-        ds[mt][r] = pv * (dpv - d4[r]);
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
+        // forward's ballots of sub-block (query 16-block, this key 16-block):
+        // ballot r holds (key 4G+r, query c) at bit 16G+c; this lane wants
+        // key c16 = 4(c16>>2) + (c16&3) for queries 4g..4g+3
+        // forward lane (G, c) of word [q16][key tile] holds (query c, key
+        // 16*mk + 4G + R) at bit 4mk + R: this lane (key c16 of 16-block
+        // k16, queries 4g..4g+3) reads words 16*(c16>>2) + 4g .. +3
+        uint32_t mbits = 0u;
+        if constexpr (use_mask) {
+          const int j = (k16 >> 2) - BX * KG, bit = (k16 & 3) * 4 + (c16 & 3);
+          const uint64_t w = *reinterpret_cast<const uint64_t*>(&s_msk[cur][mt][j][(c16 >> 2) * 16 + 4 * g]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mbits |= (uint32_t)((w >> (16 * r + bit)) & 1ull) << r;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = fast_exp2(fmaf(sacc[r], c, -l4[r]));
+          if (diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
+          float dpv = dpacc[r];
+          float pdv = pv;
+          if (DROP) {
+            bool keep;
+            if constexpr (use_mask) {
+              keep = (mbits >> r) & 1u;
+            } else {
+              const uint32_t hb = smer_pair_bits(s_rk[cur][mt * 16 + 4 * g + r], kpair);
+              keep = (khi ? (hb >> 16) : (hb & 0xFFFFu)) >= drop_thr;
+            }
+            pdv = keep ? pv * drop_scale : 0.f;
+            dpv = keep ? dpv * drop_scale : 0.f;
+          }
+          pd[mt][r] = pdv;
+          ds[mt][r] = pv * (dpv - d4[r]);
+        }
       }
+      pf[gk][0] = pack_p(pd, 0);
+      pf[gk][1] = pack_p(pd, 1);
+      sf[gk][0] = pack_p(ds, 0);
+      sf[gk][1] = pack_p(ds, 1);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 pf = pack_p(pd, ks);
-      bf16x8 sf = pack_p(ds, ks);
 #pragma unroll
       for (int dt = 0; dt < C::NDT; ++dt) {
-        adv[dt] = mfma16(tr_frag<D>(Os, ks, dt, lane), pf, adv[dt]);
-        adk[dt] = mfma16(tr_frag<D>(Qs, ks, dt, lane), sf, adk[dt]);
+        const bf16x8 of = tr_frag<D>(Os, ks, dt, lane);
+        const bf16x8 qf = tr_frag<D>(Qs, ks, dt, lane);
+#pragma unroll
+        for (int gk = 0; gk < KG; ++gk) {
+          adv[gk][dt] = mfma16(of, pf[gk][ks], adv[gk][dt]);
+          adk[gk][dt] = mfma16(qf, sf[gk][ks], adk[gk][dt]);
+        }
       }
     }
     if (more) store(cur ^ 1);
     __syncthreads();
   }
-  if (kj >= Lk) return;
-  bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
-  bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
-  // select, not multiply: a padded key's unmasked P may have overflowed
 #pragma unroll
-  for (int dt = 0; dt < C::NDT; ++dt) {
-    bf16x4 wk, wv;
+  for (int gk = 0; gk < KG; ++gk) {
+    const int kj = k0w + gk * 16 + c16;
+    if (kj >= Lk) continue;
+    bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
+    bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
+    // select, not multiply: a padded key's unmasked P may have overflowed
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      wk[r] = (bf16)(kvalid ? adk[dt][r] * scale : 0.f);
-      wv[r] = (bf16)(kvalid ? adv[dt][r] : 0.f);
+    for (int dt = 0; dt < C::NDT; ++dt) {
+      bf16x4 wk, wv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        wk[r] = (bf16)(kvalid[gk] ? adk[gk][dt][r] * scale : 0.f);
+        wv[r] = (bf16)(kvalid[gk] ? adv[gk][dt][r] : 0.f);
+      }
+      *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
+      *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
     }
-    *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
-    *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
   }
 }
 
 // ---------------------------------------------------------------------------
 // bf16 backward: dQ
 // ---------------------------------------------------------------------------
-template <int D, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
+template <int D, bool DROP, int QG, bool MSK = false>
+__global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
     const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
-    uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq) {
+    uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq,
+    const uint64_t* __restrict__ drop_mask) {
   using C = AttnCfg<D>;
+  constexpr int QB = 64 * QG;  // queries per block
+  const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
+  // forward's keep words: [query 16-block of the block][lane] for the
+  // staged key tile (16 bits each, the forward's own lane mapping)
+  __shared__ __attribute__((aligned(16))) uint16_t s_msk[2][4 * QG][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
   xcd_block2d(BX, BY);
   const int bh = BY, b = bh / H, h = bh % H;
-  const int qi = BX * 64 + wave * 16 + c16;
-  const bool qvalid = qi < Lq;
+  const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
-  bf16x8 qf[C::NS], of[C::NS];
-  {
+  constexpr bool use_mask = DROP && MSK;
+  // 16-B chunk `ch` of the block's mask words for key tile t (8 per q16)
+  auto mask_load = [&](int t, int ch) -> uint4 {
+    const int qr = ch >> 3, cc = ch & 7;
+    const int q16 = (BX * QB >> 4) + qr;
+    return q16 < nq16
+               ? reinterpret_cast<const uint4*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 8 + cc]
+               : make_uint4(0, 0, 0, 0);
+  };
+  bf16x8 qf[QG][C::NS], of[QG][C::NS];
+  float lse2[QG], dlt[QG];
+  uint32_t rowkey[QG];
+#pragma unroll
+  for (int gq = 0; gq < QG; ++gq) {
+    const int qi = q0w + gq * 16 + c16;
+    const bool qvalid = qi < Lq;
     long row = (long)(b * Lq + min(qi, Lq - 1));
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
-      of[s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
+      qf[gq][s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
+      of[gq][s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
     }
+    // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
+    lse2[gq] = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
+    dlt[gq] = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
+    rowkey[gq] = (DROP && !MSK) ? smer_rowkey(seed, (uint32_t)(bh * Lq + qi)) : 0u;
   }
-  // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
-  const float lse2 = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
-  const float dlt = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
-  const uint32_t rowkey = DROP ? smer_rowkey(seed, (uint32_t)(bh * Lq + qi)) : 0u;
   const bf16* kb = k + (long)b * Lk * ldk + h * D;
   const bf16* vb = v + (long)b * Lk * ldv + h * D;
   const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
@@ -453,12 +554,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
   };
   int n_tiles = (Lk + KVB - 1) / KVB;
   if (causal) {
-    int qmax = min(Lq, BX * 64 + 64);
+    int qmax = min(Lq, BX * QB + QB);
     n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
   }
-  f32x4 adq[C::NDT];
+  f32x4 adq[QG][C::NDT];
 #pragma unroll
-  for (int i = 0; i < C::NDT; ++i) adq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int gq = 0; gq < QG; ++gq)
+#pragma unroll
+    for (int i = 0; i < C::NDT; ++i) adq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 rk[C::CPT], rv[C::CPT];
   if (n_tiles > 0) {
     tile_load<D>(rk, kb, ldk, 0, Lk, tid);
@@ -466,70 +569,107 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_bf16(
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
     if (tid < KVB) kbias[0][tid] = key_bias(tid);
+    if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[0][0][0])[tid] = mask_load(0, tid);
   }
   __syncthreads();
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
     float nbias = 0.f;
+    uint4 nmask = make_uint4(0, 0, 0, 0);
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
       if (tid < KVB) nbias = key_bias((t + 1) * KVB + tid);
+      if (use_mask && tid < 32 * QG) nmask = mask_load(t + 1, tid);
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
-    const bool diag = causal && t * KVB + KVB - 1 > BX * 64 + wave * 16;
-    float ds[4][4];
+    f32x4 sacc[QG][4], dpacc[QG][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      f32x4 sacc = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
-      f32x4 dpacc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
+#pragma unroll
+      for (int gq = 0; gq < QG; ++gq) {
+        sacc[gq][mt] = kbv;
+        dpacc[gq][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int s = 0; s < C::NS; ++s) {
-        sacc = mfma16(row_frag<D>(Ks, mt * 16, s, lane), qf[s], sacc);
-        dpacc = mfma16(row_frag<D>(Vs, mt * 16, s, lane), of[s], dpacc);
-      }
-      float dpv[4];
+        const bf16x8 kf = row_frag<D>(Ks, mt * 16, s, lane);
+        const bf16x8 vfr = row_frag<D>(Vs, mt * 16, s, lane);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dpv[r] = dpacc[r];
-      if (DROP) {
-        const uint32_t pb = (uint32_t)(t * (KVB / 2) + mt * 8 + 2 * g);
-#pragma unroll
-        for (int rp = 0; rp < 2; ++rp) {
-          const uint32_t hb = smer_pair_bits(rowkey, pb + rp);
-          dpv[2 * rp] = (hb & 0xFFFFu) >= drop_thr ? dpv[2 * rp] * drop_scale : 0.f;
-          dpv[2 * rp + 1] = (hb >> 16) >= drop_thr ? dpv[2 * rp + 1] * drop_scale : 0.f;
+        for (int gq = 0; gq < QG; ++gq) {
+          sacc[gq][mt] = mfma16(kf, qf[gq][s], sacc[gq][mt]);
+          dpacc[gq][mt] = mfma16(vfr, of[gq][s], dpacc[gq][mt]);
         }
       }
+    }
+    bf16x8 sf[QG][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = fast_exp2(fmaf(sacc[r], c, -lse2));
-        if (diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
-        ds[mt][r] = pv * (dpv[r] - dlt);
+    for (int gq = 0; gq < QG; ++gq) {
+      const int qi = q0w + gq * 16 + c16;
+      const bool diag = causal && t * KVB + KVB - 1 > q0w + gq * 16;
+      float ds[4][4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        float dpv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dpv[r] = dpacc[gq][mt][r];
+        if constexpr (use_mask) {
+          // same lane mapping as the forward: bit 4mt + r of this lane's word
+          const uint32_t w = s_msk[cur][((q0w - BX * QB) >> 4) + gq][lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            dpv[r] = ((w >> (mt * 4 + r)) & 1u) ? dpv[r] * drop_scale : 0.f;
+        } else if (DROP) {
+          const uint32_t pb = (uint32_t)(t * (KVB / 2) + mt * 8 + 2 * g);
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) {
+            const uint32_t hb = smer_pair_bits(rowkey[gq], pb + rp);
+            dpv[2 * rp] = (hb & 0xFFFFu) >= drop_thr ? dpv[2 * rp] * drop_scale : 0.f;
+            dpv[2 * rp + 1] = (hb >> 16) >= drop_thr ? dpv[2 * rp + 1] * drop_scale : 0.f;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = fast_exp2(fmaf(sacc[gq][mt][r], c, -lse2[gq]));
+          if (diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
+          ds[mt][r] = pv * (dpv[r] - dlt[gq]);
+        }
       }
+      sf[gq][0] = pack_p(ds, 0);
+      sf[gq][1] = pack_p(ds, 1);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 sf = pack_p(ds, ks);
 #pragma unroll
-      for (int dt = 0; dt < C::NDT; ++dt) adq[dt] = mfma16(tr_frag<D>(Ks, ks, dt, lane), sf, adq[dt]);
+      for (int dt = 0; dt < C::NDT; ++dt) {
+        const bf16x8 kt = tr_frag<D>(Ks, ks, dt, lane);
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) adq[gq][dt] = mfma16(kt, sf[gq][ks], adq[gq][dt]);
+      }
     }
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
       if (tid < KVB) kbias[cur ^ 1][tid] = nbias;
+      if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[cur ^ 1][0][0])[tid] = nmask;
     }
     __syncthreads();
   }
-  if (!qvalid) return;
-  bf16* dqr = dq + (long)(b * Lq + qi) * lddq + h * D;
 #pragma unroll
-  for (int dt = 0; dt < C::NDT; ++dt) {
-    bf16x4 w;
+  for (int gq = 0; gq < QG; ++gq) {
+    const int qi = q0w + gq * 16 + c16;
+    if (qi >= Lq) continue;
+    bf16* dqr = dq + (long)(b * Lq + qi) * lddq + h * D;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) w[r] = (bf16)(adq[dt][r] * scale);
-    *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;
+    for (int dt = 0; dt < C::NDT; ++dt) {
+      bf16x4 w;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) w[r] = (bf16)(adq[gq][dt][r] * scale);
+      *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;
+    }
   }
 }
 
@@ -945,7 +1085,7 @@ template <int D>
 static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
                             long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
                             const uint8_t* kpm, int causal, float scale, uint32_t thr,
-                            uint32_t seed, float ds, hipStream_t s) {
+                            uint32_t seed, float ds, uint64_t* mask, hipStream_t s) {
   // two query groups per wave once there are enough blocks to fill the chip
   const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
   dim3 grid(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H);
@@ -953,14 +1093,23 @@ static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                   : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>);
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
-                     scale, thr, seed, ds);
+                     scale, thr, seed, ds, thr ? mask : nullptr);
+}
+
+// [bh][query 16-block][key 64-tile][64 lanes] 16-bit words: lane (g, c) of
+// the forward's wave holds (query 16*q16 + c, key 64*t + 16*mt + 4g + r) at
+// bit 4mt + r.  1 bit per (query, key).
+extern "C" size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk) {
+  return (size_t)B * H * ((Lq + 15) / 16) * ((Lk + 63) / 64) * 128;
 }
 
 extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
                              long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
                              long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
-                             float drop_p, uint32_t seed, smer_stream_t stream) {
+                             float drop_p, uint32_t seed, void* drop_mask,
+                             smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq >= 0 && Lk > 0 && D > 0, "smer_attn_fwd: bad sizes");
+  SMER_REQUIRE(!drop_mask || (((uintptr_t)drop_mask) & 15) == 0, "smer_attn_fwd: mask alignment");
   SMER_REQUIRE(q && k && v && o && lse, "smer_attn_fwd: null pointer");
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
   if (Lq == 0) return SMER_OK;
@@ -971,9 +1120,9 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
                  "smer_attn_fwd: row strides must be multiples of 8");
-    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
-    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
-    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, s);
+    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
+    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
+    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     SMER_REQUIRE((size_t)Lk * 16 <= 160 * 1024, "smer_attn_fwd(f32): Lk too large");
@@ -999,17 +1148,30 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                             long ldk, const void* v, long ldv, const void* dout, long lddo,
                             const float* lse, const float* delta, const uint8_t* kpm, int causal,
                             float scale, uint32_t thr, uint32_t seed, float ds, void* dq,
-                            long lddq, void* dk, long lddk, void* dv, long lddv, hipStream_t s) {
-  auto kdkdv = thr ? attn_bwd_dkdv_bf16<D, true> : attn_bwd_dkdv_bf16<D, false>;
-  auto kdq = thr ? attn_bwd_dq_bf16<D, true> : attn_bwd_dq_bf16<D, false>;
-  hipLaunchKernelGGL(kdkdv, dim3((Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+                            long lddq, void* dk, long lddk, void* dv, long lddv,
+                            const uint64_t* mask, hipStream_t s) {
+  if (!thr) mask = nullptr;
+  // two key groups per wave once there are enough blocks to fill the chip
+  const bool kg2 = (long)((Lk + 127) / 128) * B * H >= 512 && D <= 64;
+  // dropout variants: recompute the keep bits by hashing, or read the
+  // forward's stored bits (MSK)
+  auto kdkdv = kg2 ? (!thr ? attn_bwd_dkdv_bf16<D, false, 2>
+                      : mask ? attn_bwd_dkdv_bf16<D, true, 2, true> : attn_bwd_dkdv_bf16<D, true, 2>)
+                   : (!thr ? attn_bwd_dkdv_bf16<D, false, 1>
+                      : mask ? attn_bwd_dkdv_bf16<D, true, 1, true> : attn_bwd_dkdv_bf16<D, true, 1>);
+  const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
+  auto kdq = qg2 ? (!thr ? attn_bwd_dq_bf16<D, false, 2>
+                    : mask ? attn_bwd_dq_bf16<D, true, 2, true> : attn_bwd_dq_bf16<D, true, 2>)
+                 : (!thr ? attn_bwd_dq_bf16<D, false, 1>
+                    : mask ? attn_bwd_dq_bf16<D, true, 1, true> : attn_bwd_dq_bf16<D, true, 1>);
+  hipLaunchKernelGGL(kdkdv, dim3(kg2 ? (Lk + 127) / 128 : (Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
-                     (bf16*)dk, lddk, (bf16*)dv, lddv);
-  hipLaunchKernelGGL(kdq, dim3((Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
+                     (bf16*)dk, lddk, (bf16*)dv, lddv, mask);
+  hipLaunchKernelGGL(kdq, dim3(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
-                     (bf16*)dq, lddq);
+                     (bf16*)dq, lddq, mask);
 }
 
 extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
@@ -1018,7 +1180,7 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
                              const float* lse, const uint8_t* kpm, int causal, float scale,
                              float drop_p, uint32_t seed, void* dq, long lddq, void* dk, long lddk,
                              void* dv, long lddv, void* workspace, size_t ws_bytes,
-                             smer_stream_t stream) {
+                             const void* drop_mask, smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && D > 0, "smer_attn_bwd: bad sizes");
   SMER_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "smer_attn_bwd: null pointer");
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
@@ -1032,9 +1194,9 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
     SMER_REQUIRE(al16(q) && al16(k) && al16(v) && al16(dout), "smer_attn_bwd: 16-B alignment");
     SMER_REQUIRE(al16(o) && ldo % 8 == 0 && lddo % 8 == 0, "smer_attn_bwd: O/dO alignment");
     launch_delta<bf16>(B, H, Lq, D, o, ldo, dout, lddo, delta, s);
-    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
-    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
-    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, s);
+    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
+    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
+    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     hipLaunchKernelGGL(attn_delta_scalar<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H,

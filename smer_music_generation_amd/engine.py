@@ -216,6 +216,16 @@ class Engine:
         ctx.B, ctx.S, ctx.T, ctx.dt, ctx.p_pos, ctx.p_tr, ctx.seed = B, S, T, dt, p_pos, p_tr, seed
         ctx.src_ids, ctx.tgt_ids, ctx.skpm, ctx.tkpm, ctx.mkpm = src_ids, tgt_ids, skpm, tkpm, mkpm
         ctx.enc, ctx.dec = [], []
+        # attention-dropout keep bits written by the forward, read by backward
+        ctx.masks = {}
+        keep_mask = save and p_tr > 0 and dt == torch.bfloat16
+
+        def amask(key, Lq, Lk):
+            if not keep_mask:
+                return None
+            m_ = ops.attn_drop_mask(B, H, Lq, Lk, dev)
+            ctx.masks[key] = m_
+            return m_
 
         x = torch.empty(B * S, d, dtype=dt, device=dev)
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
@@ -224,7 +234,8 @@ class Engine:
             o = torch.empty(B * S, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, S, device=dev)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
-                         D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)))
+                         D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)),
+                         drop_mask=amask(("enc", i), S, S))
             y1 = ops.linear(o, L.out_w, L.out_b, residual=x, drop_p=p_tr, seed=sd(_site("enc", i, 1)))
             x1, m1, r1 = self._ln(y1, L.n1, dt)
             h = ops.linear(x1, L.l1_w, L.l1_b, relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
@@ -245,7 +256,8 @@ class Engine:
             o = torch.empty(B * T, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, T, device=dev)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
-                         D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)))
+                         D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)),
+                         drop_mask=amask(("dec", i), T, T))
             y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr, seed=sd(_site("dec", i, 1)))
             x1, m1, r1 = self._ln(y1, L.n1, dt)
             qc = ops.linear(x1, L.cq_w, L.cq_b)
@@ -253,7 +265,8 @@ class Engine:
             oc = torch.empty(B * T, d, dtype=dt, device=dev)
             lsec = torch.empty(B, H, T, device=dev)
             ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
-                         causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)))
+                         causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)),
+                         drop_mask=amask(("cross", i), T, S))
             if need_weights:
                 ops.attn_weights(qc, kvc[:, :d], lsec, wts[i], B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                                  scale=scale)
@@ -325,7 +338,7 @@ class Engine:
             dkvc = torch.empty(Ms, 2 * d, dtype=dt, device=dev)
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
-                         drop_p=p_tr, seed=sd(_site("dec", i, 2)))
+                         drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)))
             dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
             ops.linear_wgrad(dqc, x1, GL.cq_w, db=GL.cq_b)
             ops.linear_dgrad(dkvc, L.ckv_w, out_f32=dmem, accumulate=True)
@@ -341,7 +354,7 @@ class Engine:
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
-                         seed=sd(_site("dec", i, 0)))
+                         seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)))
             dy = ops.linear_dgrad(dqkv, L.sa_w, residual=dy1)
             ops.linear_wgrad(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             if hook:
@@ -373,7 +386,7 @@ class Engine:
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
-                         seed=sd(_site("enc", i, 0)))
+                         seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)))
             dx = ops.linear_dgrad(dqkv, L.in_w, residual=dy1)
             ops.linear_wgrad(dqkv, x_in, GL.in_w, db=GL.in_b)
             if hook:

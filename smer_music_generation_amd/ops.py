@@ -164,15 +164,21 @@ def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None):
 
 
 # ---------------------------------------------------------------------------
+def attn_drop_mask(B, H, Lq, Lk, device):
+    """Buffer for the forward's attention-dropout keep bits (read by attn_bwd)."""
+    n = load().smer_attn_drop_mask_bytes(B, H, Lq, Lk)
+    return torch.empty(max(16, n), dtype=torch.uint8, device=device)
+
+
 def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale, drop_p=0.0,
-             seed=0):
+             seed=0, drop_mask=None):
     call("smer_attn_fwd", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k),
          _p(v), _ld(v), _p(o), _ld(o), _p(lse), _p(kpm), int(causal), float(scale),
-         float(drop_p), int(seed) & 0xFFFFFFFF, _stream())
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(drop_mask), _stream())
 
 
 def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, causal=False,
-             scale, drop_p=0.0, seed=0):
+             scale, drop_p=0.0, seed=0, drop_mask=None):
     lib = load()
     dt = dtype_code(q.dtype)
     nbytes = lib.smer_attn_bwd_workspace(dt, B, H, Lq, Lk)
@@ -180,7 +186,7 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, caus
     call("smer_attn_bwd", dt, B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v),
          _p(o), _ld(o), _p(do), _ld(do), _p(lse), _p(kpm), int(causal), float(scale),
          float(drop_p), int(seed) & 0xFFFFFFFF, _p(dq), _ld(dq), _p(dk), _ld(dk), _p(dv),
-         _ld(dv), _p(ws), nbytes, _stream())
+         _ld(dv), _p(ws), nbytes, _p(drop_mask), _stream())
 
 
 def attn_weights(q, k, lse, out, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale):

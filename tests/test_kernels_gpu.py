@@ -252,8 +252,9 @@ def test_attention_dropout(dtype, B, H, L, causal):
     keep = torch.from_numpy(attn_keep_mask(seed, p, B * H * L, L)).to(dev).view(B, H, L, L)
     o = torch.empty(B * L, H * D, device=dev, dtype=dtype)
     lse = torch.empty(B, H, L, device=dev)
+    mask = O.attn_drop_mask(B, H, L, L, dev)
     O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal, scale=scale,
-               drop_p=p, seed=seed)
+               drop_p=p, seed=seed, drop_mask=mask)
     qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, k, v))
     ro, _ = attn_ref(qf, kf, vf, B, H, L, L, D, kpm, causal, scale, keep, p)
     torch.cuda.synchronize()
@@ -270,6 +271,13 @@ def test_attention_dropout(dtype, B, H, L, causal):
     tolb = 4e-2 if dtype == torch.bfloat16 else 1e-4
     for a, b in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         assert rel_err(a, b) < tolb
+    if dtype == torch.bfloat16:
+        # backward reading the forward's stored keep bits == re-hashing
+        dq2, dk2, dv2 = torch.empty_like(dq), torch.empty_like(dk), torch.empty_like(dv)
+        O.attn_bwd(q, k, v, o, do, lse, dq2, dk2, dv2, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm,
+                   causal=causal, scale=scale, drop_p=p, seed=seed, drop_mask=mask)
+        torch.cuda.synchronize()
+        assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -445,3 +453,30 @@ def test_adam_and_cast_and_colsum():
     O.cast(x, xb)
     torch.cuda.synchronize()
     assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(2, 2, 96, 96, True), (2, 2, 80, 150, False),
+                                              (16, 8, 512, 512, False)])
+def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
+    """The forward's stored keep bits equal tests/hashref.keep_mask: 16-bit
+    words [bh][q16][key tile t][lane = 16g + c], bit 4mt + r = (query
+    16*q16 + c, key 64t + 16mt + 4g + r)."""
+    O = ops()
+    D, p, seed = 64, 0.1, 99
+    q, k, v, _ = _attn_inputs(B, H, Lq, Lk, D, torch.bfloat16, False)
+    o = torch.empty(B * Lq, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, Lq, device=dev)
+    mask = O.attn_drop_mask(B, H, Lq, Lk, dev)
+    mask.zero_()
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=0.125,
+               drop_p=p, seed=seed, drop_mask=mask)
+    torch.cuda.synchronize()
+    nq, nt = (Lq + 15) // 16, (Lk + 63) // 64
+    w = mask[: B * H * nq * nt * 128].cpu().numpy().view(np.uint16).reshape(B * H, nq, nt, 4, 16)
+    bits = (w[..., None].astype(np.uint32) >> np.arange(16, dtype=np.uint32)) & 1  # [bh,q16,t,g,c,16]
+    bits = bits.reshape(B * H, nq, nt, 4, 16, 4, 4)                                  # [.., g, c, mt, r]
+    got = bits.transpose(0, 1, 4, 2, 5, 3, 6).reshape(B * H, nq * 16, nt * 64)       # [bh, q, key]
+    ref = keep_mask(seed, p, B * H * Lq, Lk).reshape(B * H, Lq, Lk)
+    sel = np.ones((Lq, Lk), bool) if not causal else np.tril(np.ones((Lq, Lk), bool))
+    g = got[:, :Lq, :Lk].astype(bool)
+    assert (g[:, sel] == ref[:, sel]).all()

@@ -88,8 +88,10 @@ def bench_attn():
         sc = 1 / math.sqrt(D)
         t = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D,
                                         causal=causal, scale=sc))
+        msk = ops.attn_drop_mask(B, H, Lq, Lk, dev)
         td = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D,
-                                         causal=causal, scale=sc, drop_p=0.1, seed=1))
+                                         causal=causal, scale=sc, drop_p=0.1, seed=1,
+                                         drop_mask=msk))
         do = torch.randn_like(o)
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
@@ -97,7 +99,7 @@ def bench_attn():
                                          B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=sc))
         tbd = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, dq, dkv[:, :H * D], dkv[:, H * D:],
                                           B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=sc,
-                                          drop_p=0.1, seed=1))
+                                          drop_p=0.1, seed=1, drop_mask=msk))
         fl = 4.0 * B * H * Lq * Lk * D * (0.5 if causal else 1.0)
         print("%-9s fwd %8.1f us %6.1f TF | fwd+drop %8.1f us | bwd %8.1f us %6.1f TF (2.5x fwd flops)"
               " | bwd+drop %8.1f us" % (name, t, fl / t / 1e6, td, tb, 2.5 * fl / tb / 1e6, tbd))
