@@ -391,6 +391,161 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
+// 256x256 bf16 GEMM for the large-M forward (NT) and dgrad (NN) shapes.
+// 8 waves (2 along M x 4 along N), 128x64 outputs per wave: per 32-deep
+// k-step a wave reads 8 A + 4 B fragments for 32 MFMAs, and per K tile the
+// workgroup pulls 64 KiB for 8.4 MFLOP (half the L2->CU bytes per flop of
+// the 128x128 tile).  Two 64 KiB LDS stages filled by LDS-DMA one K tile
+// ahead, one barrier per K tile, one workgroup per CU (persistent).
+// Epilogue: four 64-row passes through LDS, 8-column vectors.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int G2 = 256, G2K = 64;
+constexpr int G2_OP = G2 * G2K * 2;     // 32 KiB per operand per stage
+constexpr int G2_STAGE = 2 * G2_OP;     // 64 KiB
+
+// LDS image of one operand stage: KC (row image): row r at r*128 B, 16-B
+// chunks XOR (r & 7); column image: k-row at k*512 B, 8-B units XOR
+// 4*col_swz(k) (same bank behaviour as the 256-B rows of the 128 kernel).
+template <bool KC>
+__device__ __forceinline__ void g2_glds(char* buf, const bf16* P, long ld, int rows, int r0,
+                                        int k0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int chunk = wave * 4 + c;  // 32 x 1 KiB
+    const bf16* src;
+    if (KC) {
+      const int row = chunk * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (row & 7);
+      src = P + (long)min(r0 + row, rows - 1) * ld + k0 + lc * 8;
+    } else {
+      const int k = chunk * 2 + (lane >> 5);
+      const int lc = (lane & 31) ^ (2 * (int)col_swz(k));
+      const int col = min(r0 + lc * 8, ((rows + 7) & ~7) - 8);
+      src = P + (long)(k0 + k) * ld + col;
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
+  }
+}
+template <bool KC>
+__device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int lane) {
+  const int g = lane >> 4, c16 = lane & 15;
+  if (KC) {
+    const int row = rbase + c16;
+    const int ch = s * 4 + g;
+    return lds_read_b128(buf, row * 128 + ((ch ^ (row & 7)) << 4));
+  } else {
+    const int q = c16 >> 2, p = c16 & 3;
+    const int u = (rbase >> 2) + p;
+    const int k0 = s * 32 + 8 * g + q;
+    const int k1 = k0 + 4;
+    bf16x4 lo = lds_read_tr16(buf, k0 * 512 + ((u ^ (4 * col_swz(k0))) << 3));
+    bf16x4 hi = lds_read_tr16(buf, k1 * 512 + ((u ^ (4 * col_swz(k1))) << 3));
+    return cat4(lo, hi);
+  }
+}
+}  // namespace
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int K,
+                                                              const bf16* __restrict__ A, long lda,
+                                                              const bf16* __restrict__ B, long ldb,
+                                                              GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbm = (M + G2 - 1) / G2, nbn = (N + G2 - 1) / G2;
+  const int nwg = nbm * nbn;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  const int nk = K / G2K;
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int wgid = xstart + jj;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int m0 = (first_m + within % gsz) * G2, n0 = (within / gsz) * G2;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    g2_glds<AK>(smem, A, lda, M, m0, 0, tid);
+    g2_glds<BKC>(smem + G2_OP, B, ldb, N, n0, 0, tid);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // stage kt landed (vmcnt(0) + barrier); stage kt-1 fully read
+      if (kt + 1 < nk) {
+        char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
+        g2_glds<AK>(nb, A, lda, M, m0, (kt + 1) * G2K, tid);
+        g2_glds<BKC>(nb + G2_OP, B, ldb, N, n0, (kt + 1) * G2K, tid);
+      }
+      const char* a_s = smem + (kt & 1) * G2_STAGE;
+      const char* b_s = a_s + G2_OP;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 bfr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const bf16x8 af = g2_frag<AK>(a_s, wm * 128 + i * 16, s, lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
+        }
+      }
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+
+    // epilogue: 4 passes of 64 rows x 256 columns (fp32 in LDS)
+    const int g = lane >> 4, c16 = lane & 15;
+    constexpr int EP_LD = G2 + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      // rows [64*pass, 64*pass+64) belong to wm = pass >> 1, fragments
+      // i = 4*(pass & 1) .. +3
+      if (wm == (pass >> 1)) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = 4 * (pass & 1) + ii;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
+        const int row = item >> 5, ch = item & 31;
+        const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
+        if (grow < M && gcol < N) {
+          float v[8];
+          const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+          const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          epi_apply8(e, M, N, grow, gcol, v);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Skinny bf16 NT GEMM (M <= 256: decode steps, tiny batches).  The 128x128
 // tile kernel would run 4-16 workgroups there; this one gives each
 // workgroup a 64-row x 16-column output strip and splits K over its 8 waves.
@@ -564,6 +719,16 @@ static bool smer_gemm_glds_enabled() {
   return v == 1;
 }
 
+// SMER_GEMM256=0 keeps every shape on the 128x128 kernel (A/B, tests).
+static bool smer_gemm256_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_GEMM256");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static int smer_num_cus() {
   static int cache[64] = {0};
   int dev = 0;
@@ -601,6 +766,22 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     hipLaunchKernelGGL(gemm_skinny_bf16_kernel, dim3((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM),
                        dim3(64 * SK_WAVES), 0, s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
     return;
+  }
+  // large-M forward / dgrad: 256x256 tiles when they fill the chip
+  if (AK && !rowsum && K % G2K == 0 && smer_gemm256_enabled()) {
+    const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
+    if (t2 >= smer_num_cus()) {
+      const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
+      static bool attr_set = false;  // > 64 KiB dynamic LDS must be opted into
+      if (!attr_set) {
+        hipFuncSetAttribute((const void*)gemm256_bf16_kernel<AK, BKC>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G2_STAGE);
+        attr_set = true;
+      }
+      hipLaunchKernelGGL((gemm256_bf16_kernel<AK, BKC>), dim3(grid), dim3(512), 2 * G2_STAGE, s,
+                         M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+      return;
+    }
   }
   int tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   int split = choose_split(M, N, K, e, ws ? ws_bytes : 0);

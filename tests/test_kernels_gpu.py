@@ -105,6 +105,31 @@ def test_gemm_wgrad_bias(M, N, K, acc):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,N,K,bk", [(8300, 2056, 512, True), (8192, 2048, 192, False),
+                                      (16384, 1536, 1024, True), (8200, 2048, 256, False)])
+def test_gemm256_large_m(M, N, K, bk):
+    """The 256x256 kernel (>= one tile per CU) with ragged M / N tails and
+    the full epilogue (bias, relu, dropout, residual) against fp32."""
+    O = ops()
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    Wm = W if bk else W.t().contiguous()
+    bias = torch.randn(N, device=dev)
+    R = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    p, seed = 0.1, 7
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, bias=bias, relu=True, residual=R, drop_p=p,
+           seed=seed)
+    base = A.float() @ W.float().t()
+    keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
+    Cf = torch.empty(M, N, device=dev)
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out_f32=Cf)
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 2e-2
+    assert rel_err(Cf, base) < 2e-3
+
+
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128
