@@ -22,6 +22,13 @@
  *   smer_attn_decode     KV-cached single-step attention for the infill loop
  *                        (replaces the full recompute of generation.py:217)
  *   smer_kv_scatter      append new K/V rows to a per-request cache
+ *   smer_linear_decode   decode-step Linear (M <= 256 rows) whose epilogue
+ *                        also appends the new K/V columns to the cache
+ *                        (transformer.py:459 per generated token)
+ *   smer_grammar_greedy_step  the greedy infill grammar loop on device:
+ *                        state -> mask -> argmax -> commit -> next feed
+ *                        (generation.py:528-687 with weighted_sampling as
+ *                        argmax; replaces the per-token host round trip)
  *   smer_layernorm_*     residual LayerNorm, eps 1e-5 (transformer.py:392,395,
  *                        462,466,469; final norms 274-275, 329-330)
  *   smer_embed_*         embedding gather x sqrt(d) + sinusoidal PE + dropout
@@ -126,6 +133,30 @@ int smer_attn_decode(int dtype, int n_rows, int H, int D, const void* q, long ld
 int smer_kv_scatter(int dtype, int n_rows, int width, const void* src, long lds,
                     void* cache, long row_stride, long req_stride,
                     const int32_t* row_req, const int32_t* row_pos, smer_stream_t stream);
+/* Decode Linear (M <= 256 rows, bf16): C[M,N] (or fp32 Cf) = A W^T + bias
+ * (+ReLU) (+residual); kv (optional): output columns >= kv_col0 are also
+ * written to kv[kv_req[m]*kv_req_stride + kv_pos[m]*kv_row_stride + col -
+ * kv_col0] (the new token's self-attention K/V appended to the cache). */
+int smer_linear_decode(int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                       const float* bias, int relu, const void* residual, long ldr, void* C,
+                       long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
+                       long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
+                       int kv_col0, smer_stream_t stream);
+/* One greedy grammar step for R requests (generation.py:528-687).
+ * logits: fp32 [2R, >=V] rows (request r's last fed token at row 2r+1).
+ * state: int32 [R, nst>=9] = pos, flags(sep|cont<<1|pitch<<2|rest<<3), span
+ * length, mask index, n_masks, done, no_whole, emitted count, error.
+ * targets: int8 [R, max_masks] control target per mask (0 r,1 d,2 o,3 p,4 t).
+ * keep: uint8 [13, V] sampling masks per grammar state; cls: uint8 [V] token
+ * class bits (1 continue, 2 pitch, 4 duration-only, 8 'sep', 16 'rest',
+ * 32 control).  Writes the next step's ids int64 [2R] and meta int32
+ * [4, 2R] (position, request, self keys, cross keys; unused rows go to
+ * trash_pos), appends the id to out_tok [R, cap], stores #live in *alive. */
+int smer_grammar_greedy_step(int R, int V, const float* logits, long ldl, int32_t* state,
+                             int nst, const int8_t* targets, int max_masks, const uint8_t* keep,
+                             const uint8_t* cls, int eos, int m0, int trash_pos, int max_span,
+                             const int32_t* src_len, int64_t* ids, int32_t* meta,
+                             int32_t* out_tok, int cap, int32_t* alive, smer_stream_t stream);
 
 int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long ldx,
                        const float* gamma, const float* beta, float eps,

@@ -39,6 +39,10 @@ SIGNATURES = {
     "smer_attn_decode": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, P,
                                  P, P, c_long, c_float, P]),
     "smer_kv_scatter": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, c_long, P, P, P]),
+    "smer_linear_decode": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
+                                   P, c_long, P, c_long, P, c_long, c_long, P, P, c_int, P]),
+    "smer_grammar_greedy_step": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P, c_int,
+                                         c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "smer_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
                                    P, P]),
     "smer_layernorm_bwd_workspace": (c_size, [c_int, c_int]),

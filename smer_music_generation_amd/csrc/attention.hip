@@ -953,70 +953,87 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(int H, int D, const T*
 }
 
 // Vectorised single-pass decode attention (online softmax).  One block per
-// (row, head), 4 waves.  LPK lanes own one key (each lane a 16-B slice of
+// (row, head), NW waves.  LPK lanes own one key (each lane a 16-B slice of
 // D = LPK*VEC), so a wave walks 64/LPK keys per step with 16-B K and V
-// loads; UNR steps are issued together to keep loads in flight.  Each lane
-// group keeps a running (max, sum, acc[VEC]); groups are merged with
-// shuffles, waves through LDS.
+// loads; UNR steps are issued together (raw 16-B registers, converted at
+// use) so that NW * UNR * 2 KiB of K/V per block are in flight — the cross
+// attention over a 1-4k-token memory is HBM-latency bound otherwise.  The
+// UNR keys of a step update the running (max, sum, acc[VEC]) of a lane
+// group with ONE rescale; groups are merged with shuffles, waves via LDS.
 template <typename T>
-__device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) {
+__device__ __forceinline__ void cvt16b(const uint4& r, float (&v)[16 / sizeof(T)]) {
   if constexpr (sizeof(T) == 2) {
-    const bf16x8 t = *reinterpret_cast<const bf16x8*>(p);
+    const bf16x8 t = __builtin_bit_cast(bf16x8, r);
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = (float)t[i];
   } else {
-    const float4 t = *reinterpret_cast<const float4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    v[0] = __uint_as_float(r.x); v[1] = __uint_as_float(r.y);
+    v[2] = __uint_as_float(r.z); v[3] = __uint_as_float(r.w);
   }
 }
-template <typename T, int LPK, int UNR>
-__global__ __launch_bounds__(256) void attn_decode_vec_kernel(
+template <typename T>
+__device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) {
+  cvt16b<T>(*reinterpret_cast<const uint4*>(p), v);
+}
+template <typename T, int LPK, int UNR, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
     long row_stride, long req_stride, const int32_t* __restrict__ row_req,
     const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale) {
   constexpr int VEC = 16 / sizeof(T);
-  constexpr int D = LPK * VEC;
   constexpr int GPW = 64 / LPK;  // key groups per wave
-  constexpr int KPB = 4 * GPW;   // keys per block step
-  __shared__ float red_m[4][LPK], red_l[4][LPK], red_a[4][LPK][VEC];
+  constexpr int KPB = NW * GPW;  // keys per block step
+  __shared__ float red_m[NW][LPK], red_l[NW][LPK], red_a[NW][LPK][VEC];
   const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int sub = lane % LPK, grp = wave * GPW + lane / LPK;
   const int nk = row_nkeys[r];
-  const long base = (long)row_req[r] * req_stride + h * D + sub * VEC;
+  const long base = (long)row_req[r] * req_stride + h * (LPK * VEC) + sub * VEC;
   float qv[VEC];
-  load16b<T>(q + (long)r * ldq + h * D + sub * VEC, qv);
+  load16b<T>(q + (long)r * ldq + h * (LPK * VEC) + sub * VEC, qv);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) qv[i] *= scale;
   float m = -INFINITY, l = 0.f, acc[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
   for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
-    float kv[UNR][VEC], vv[UNR][VEC];
+    uint4 kr[UNR], vr[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int j = j0 + u * KPB + grp;
-      const bool ok = j < nk;
-      const long off = base + (long)(ok ? j : 0) * row_stride;
-      load16b<T>(kc + off, kv[u]);
-      load16b<T>(vc + off, vv[u]);
+      const long off = base + (long)(j < nk ? j : 0) * row_stride;
+      kr[u] = *reinterpret_cast<const uint4*>(kc + off);
+      vr[u] = *reinterpret_cast<const uint4*>(vc + off);
     }
+    float sc[UNR];
+    float mx = m;
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int j = j0 + u * KPB + grp;
+      float kv[VEC];
+      cvt16b<T>(kr[u], kv);
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) s = fmaf(qv[i], kv[u][i], s);
+      for (int i = 0; i < VEC; ++i) s = fmaf(qv[i], kv[i], s);
 #pragma unroll
       for (int w = 1; w < LPK; w <<= 1) s += __shfl_xor(s, w, 64);
-      if (j < nk) {
-        const float mn = fmaxf(m, s);
-        const float c = __expf(m - mn), p = __expf(s - mn);
-        l = l * c + p;
+      sc[u] = (j0 + u * KPB + grp) < nk ? s : -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+    if (mx != -INFINITY) {  // group-uniform: some key of this step is valid
+      const float c = __expf(m - mx);
+      l *= c;
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(acc[i], c, p * vv[u][i]);
-        m = mn;
+      for (int i = 0; i < VEC; ++i) acc[i] *= c;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const float p = __expf(sc[u] - mx);
+        float vv[VEC];
+        cvt16b<T>(vr[u], vv);
+        l += p;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(p, vv[i], acc[i]);
       }
+      m = mx;
     }
   }
   // merge the groups of a wave (lanes with equal `sub`)
@@ -1041,19 +1058,19 @@ __global__ __launch_bounds__(256) void attn_decode_vec_kernel(
   if (tid < LPK) {
     float mm = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) mm = fmaxf(mm, red_m[w][tid]);
+    for (int w = 0; w < NW; ++w) mm = fmaxf(mm, red_m[w][tid]);
     float ll = 0.f, out[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) out[i] = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float c = red_m[w][tid] == -INFINITY ? 0.f : __expf(red_m[w][tid] - mm);
       ll += red_l[w][tid] * c;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) out[i] += red_a[w][tid][i] * c;
     }
     const float inv = ll > 0.f ? 1.f / ll : 0.f;
-    T* op = o + (long)r * ldo + h * D + tid * VEC;
+    T* op = o + (long)r * ldo + h * (LPK * VEC) + tid * VEC;
     if constexpr (sizeof(T) == 2) {
       bf16x8 t;
 #pragma unroll
@@ -1262,10 +1279,19 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
     const int lpk = D / vec;
     hipStream_t s = (hipStream_t)stream;
     dim3 grid(n_rows, H);
-#define SMER_DEC_VEC(T, L)                                                                       \
-  hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 2>), grid, dim3(256), 0, s, (const T*)q, ldq, \
-                     (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,          \
-                     row_nkeys, (T*)o, ldo, scale)
+    // key capacity of a request (cache rows): long memories get 8 waves x
+    // 4 steps of loads in flight per block, short self-attention caches 4 x 2
+    const long cap_rows = req_stride / (row_stride > 0 ? row_stride : 1);
+    const bool big = cap_rows >= 512;
+#define SMER_DEC_VEC(T, L)                                                                        \
+  if (big)                                                                                        \
+    hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8>), grid, dim3(512), 0, s, (const T*)q,  \
+                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,   \
+                       row_nkeys, (T*)o, ldo, scale);                                             \
+  else                                                                                            \
+    hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 2, 4>), grid, dim3(256), 0, s, (const T*)q,  \
+                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,   \
+                       row_nkeys, (T*)o, ldo, scale)
     if (ok && (lpk == 4 || lpk == 8 || lpk == 16)) {
       if (dtype == SMER_BF16) {
         if (lpk == 4) SMER_DEC_VEC(bf16, 4); else if (lpk == 8) SMER_DEC_VEC(bf16, 8); else SMER_DEC_VEC(bf16, 16);

@@ -18,7 +18,7 @@ PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "libsmer_hip.so")
 OBJ = os.path.join(HERE, "_build")
-SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm_embed.hip", "train_ops.hip"]
+SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm_embed.hip", "train_ops.hip", "decode_ops.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "smer_hip.h")]
 ARCH = os.environ.get("SMER_OFFLOAD_ARCH", "gfx950")
 

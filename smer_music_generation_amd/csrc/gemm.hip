@@ -33,6 +33,13 @@ struct GemmEpi {
   int accumulate;
   int vec;  // every operand 16-B aligned with row strides % 8 == 0
   int rs_accumulate;  // fused row-sum output (bias gradient) accumulates
+  // decode: columns >= kv_col0 are also appended to a per-request K/V cache
+  // at kv[kv_req[row] * kv_req_stride + kv_pos[row] * kv_row_stride + col - kv_col0]
+  void* kv;
+  long kv_row_stride, kv_req_stride;
+  const int32_t* kv_req;
+  const int32_t* kv_pos;
+  int kv_col0;
 };
 
 template <typename T>
@@ -53,6 +60,9 @@ __device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int ro
     float* p = e.Cf + (long)row * e.ldcf + col;
     *p = e.accumulate ? *p + v : v;
   }
+  if (e.kv && col >= e.kv_col0)
+    ((T*)e.kv)[(long)e.kv_req[row] * e.kv_req_stride + (long)e.kv_pos[row] * e.kv_row_stride +
+               (col - e.kv_col0)] = from_f32<T>(v);
 }
 
 // Eight consecutive columns of one row (bf16 activations).  Vector path when
@@ -88,11 +98,14 @@ __device__ __forceinline__ void epi_apply8(const GemmEpi& e, int M, int N, int r
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = (float)gt[k] > 0.f ? v[k] * e.gate_scale : 0.f;
   }
-  if (e.C) {
+  if (e.C || e.kv) {
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-    *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)row * e.ldc + col) = o;
+    if (e.C) *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)row * e.ldc + col) = o;
+    if (e.kv && col >= e.kv_col0)  // kv_col0 % 8 == 0: a chunk is all K/V or all Q
+      *reinterpret_cast<bf16x8*>((bf16*)e.kv + (long)e.kv_req[row] * e.kv_req_stride +
+                                 (long)e.kv_pos[row] * e.kv_row_stride + (col - e.kv_col0)) = o;
   }
   if (e.Cf) {
     float* p = e.Cf + (long)row * e.ldcf + col;
@@ -555,18 +568,80 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
 // the shared epilogue runs on 8-column vectors.
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int SK_BM = 64, SK_BN = 16, SK_WAVES = 8, SK_UNR = 2;
+constexpr int SK_BM = 64, SK_BN = 16;
 }
-__global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int K,
-                                                               const bf16* __restrict__ A, long lda,
-                                                               const bf16* __restrict__ B, long ldb,
-                                                               GemmEpi e) {
-  __shared__ float red[SK_WAVES][SK_BM][SK_BN + 1];
+// The epilogue's bias / residual for one 8-column chunk, loaded BEFORE the K
+// loop so that their HBM latency overlaps the operand loads (a decode-step
+// GEMM is a handful of dependent memory round trips; this removes one).
+struct EpiPre {
+  float b[8];
+  float r[8];
+};
+__device__ __forceinline__ bool epi_pre_ok(const GemmEpi& e, int M, int N, int row, int col) {
+  return e.vec && row < M && col + 8 <= N;
+}
+__device__ __forceinline__ void epi_prefetch(const GemmEpi& e, int row, int col, EpiPre& p) {
+  if (e.bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col);
+    const float4 b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
+    p.b[0] = b0.x; p.b[1] = b0.y; p.b[2] = b0.z; p.b[3] = b0.w;
+    p.b[4] = b1.x; p.b[5] = b1.y; p.b[6] = b1.z; p.b[7] = b1.w;
+  }
+  if (e.residual) {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)row * e.ldr + col);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.r[k] = (float)r[k];
+  }
+}
+// epi_apply8 with the prefetched bias / residual (vector path only)
+__device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int col, float (&v)[8],
+                                               const EpiPre& p) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
+  if (e.bias) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += p.b[k];
+  }
+  if (e.relu) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  if (e.drop_thr) smer_drop8(smer_rowkey(e.seed, (uint32_t)row), e.drop_thr, e.drop_scale, (uint32_t)col, v);
+  if (e.residual) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += p.r[k];
+  }
+  GemmEpi e2 = e;  // the rest (gate, stores) through the shared path
+  e2.alpha = 1.f; e2.bias = nullptr; e2.relu = 0; e2.drop_thr = 0; e2.residual = nullptr;
+  epi_apply8(e2, row + 1, col + 8, row, col, v);
+}
+
+// Skinny bf16 NT GEMM (M <= 256: decode steps, tiny batches).  The 128x128
+// tile kernel would run 4-16 workgroups there; this one gives each
+// workgroup a 64-row x 16-column output strip and splits K over its NW
+// waves, UNR 32-deep K steps per wave issued together (NW * UNR * 32 >= K
+// in the decode shapes: one round of loads).  MFMA fragments are loaded
+// straight from global memory (both operands K-contiguous: one 16-B load
+// per lane per fragment); the NW partial tiles are summed through LDS in
+// fixed order (deterministic), then the epilogue runs on 8-column vectors
+// with its bias / residual already in registers.
+template <int NW, int UNR>
+__global__ __launch_bounds__(64 * NW) void gemm_skinny_bf16_kernel(int M, int N, int K,
+                                                                   const bf16* __restrict__ A, long lda,
+                                                                   const bf16* __restrict__ B, long ldb,
+                                                                   GemmEpi e) {
+  __shared__ float red[NW][SK_BM][SK_BN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * SK_BN, m0 = blockIdx.y * SK_BM;
   const int r16 = lane & 15, kq = (lane >> 4) * 8;
   const int ncol = n0 + r16;
   const bool colok = ncol < N;
+  // epilogue chunk of this thread (tid < 128: row tid/2, 8 columns)
+  const int erow = m0 + (tid >> 1), ecol = n0 + (tid & 1) * 8;
+  const bool eth = tid < SK_BM * 2;
+  const bool pre = eth && epi_pre_ok(e, M, N, erow, ecol);
+  EpiPre ep;
+  if (pre) epi_prefetch(e, erow, ecol, ep);
   const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
   const bf16* ap[4];
   bool rowok[4];
@@ -580,11 +655,11 @@ __global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nsteps = (K + 31) / 32;
-  for (int s0 = wave; s0 < nsteps; s0 += SK_WAVES * SK_UNR) {
-    bf16x8 a[SK_UNR][4], b[SK_UNR];
+  for (int s0 = wave; s0 < nsteps; s0 += NW * UNR) {
+    bf16x8 a[UNR][4], b[UNR];
 #pragma unroll
-    for (int u = 0; u < SK_UNR; ++u) {
-      const int k = (s0 + u * SK_WAVES) * 32;
+    for (int u = 0; u < UNR; ++u) {
+      const int k = (s0 + u * NW) * 32;
       const bool kok = k + kq < K;  // K % 8 == 0: a lane's 8-chunk is all in or all out
       b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
 #pragma unroll
@@ -592,7 +667,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int
         a[u][i] = (rowok[i] && kok) ? *reinterpret_cast<const bf16x8*>(ap[i] + k) : bf16x8{};
     }
 #pragma unroll
-    for (int u = 0; u < SK_UNR; ++u)
+    for (int u = 0; u < UNR; ++u)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
   }
@@ -603,19 +678,19 @@ __global__ __launch_bounds__(512) void gemm_skinny_bf16_kernel(int M, int N, int
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][i * 16 + 4 * g + r][r16] = acc[i][r];
   __syncthreads();
-  if (tid < SK_BM * 2) {
+  if (eth) {
     const int row = tid >> 1, ch = tid & 1;
-    const int grow = m0 + row, gcol = n0 + ch * 8;
-    if (grow < M && gcol < N) {
+    if (erow < M && ecol < N) {
       float v[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         float t = 0.f;
 #pragma unroll
-        for (int w = 0; w < SK_WAVES; ++w) t += red[w][row][ch * 8 + c];
+        for (int w = 0; w < NW; ++w) t += red[w][row][ch * 8 + c];
         v[c] = t;
       }
-      epi_apply8(e, M, N, grow, gcol, v);
+      if (pre) epi_apply8_pre(e, erow, ecol, v, ep);
+      else epi_apply8(e, M, N, erow, ecol, v);
     }
   }
 }
@@ -763,8 +838,14 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                         const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s,
                         float* rowsum = nullptr) {
   if (AK && BKC && M <= 4 * SK_BM && !rowsum) {
-    hipLaunchKernelGGL(gemm_skinny_bf16_kernel, dim3((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM),
-                       dim3(64 * SK_WAVES), 0, s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+    const dim3 grid((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM);
+    const int nsteps = (K + 31) / 32;
+    if (nsteps > 16)  // 8 waves x 4 steps (16 waves would spill at 128 VGPRs)
+      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 4>), grid, dim3(512), 0, s, M, N, K,
+                         (const bf16*)A, lda, (const bf16*)B, ldb, e);
+    else
+      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 2>), grid, dim3(512), 0, s, M, N, K,
+                         (const bf16*)A, lda, (const bf16*)B, ldb, e);
     return;
   }
   // large-M forward / dgrad: 256x256 tiles when they fill the chip
@@ -829,7 +910,7 @@ extern "C" int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, 
   SMER_REQUIRE(C || Cf, "smer_gemm: no output");
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_gemm: drop_p out of range");
   if (M == 0 || N == 0) return SMER_OK;
-  GemmEpi e;
+  GemmEpi e{};
   e.bias = bias; e.alpha = alpha; e.relu = relu; e.residual = residual; e.ldr = ldr;
   e.gate = gate; e.ldg = ldg; e.gate_scale = gate_scale;
   e.drop_thr = smer_drop_thr16(drop_p); e.seed = drop_seed;
@@ -884,5 +965,29 @@ extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* 
   e.vec = a16(dW, lddw);
   launch_bf16<false, false>(M, N, K, dy, lddy, x, ldx, e, workspace, ws_bytes, (hipStream_t)stream, db);
   SMER_CHECK_LAUNCH("smer_gemm_wgrad_bias");
+  return SMER_OK;
+}
+
+extern "C" int smer_linear_decode(int M, int N, int K, const void* A, long lda, const void* W,
+                                  long ldw, const float* bias, int relu, const void* residual,
+                                  long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
+                                  long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
+                                  const int32_t* kv_pos, int kv_col0, smer_stream_t stream) {
+  SMER_REQUIRE(M > 0 && M <= 4 * SK_BM && N > 0 && K > 0, "smer_linear_decode: sizes (M <= 256)");
+  SMER_REQUIRE(A && W && (C || Cf), "smer_linear_decode: null operand");
+  SMER_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldw % 8 == 0 && aligned16(A) && aligned16(W),
+               "smer_linear_decode: K / strides / alignment");
+  SMER_REQUIRE(!kv || (kv_req && kv_pos && kv_col0 % 8 == 0 && kv_col0 >= 0 && kv_col0 < N &&
+                       aligned16(kv) && kv_row_stride % 8 == 0 && kv_req_stride % 8 == 0),
+               "smer_linear_decode: kv scatter arguments");
+  GemmEpi e{};
+  e.bias = bias; e.alpha = 1.f; e.relu = relu; e.residual = residual; e.ldr = ldr;
+  e.drop_scale = 1.f; e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf;
+  e.kv = kv; e.kv_row_stride = kv_row_stride; e.kv_req_stride = kv_req_stride;
+  e.kv_req = kv_req; e.kv_pos = kv_pos; e.kv_col0 = kv_col0;
+  auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
+  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc) && a16(Cf, ldcf);
+  launch_bf16<true, true>(M, N, K, A, lda, W, ldw, e, nullptr, 0, (hipStream_t)stream);
+  SMER_CHECK_LAUNCH("smer_linear_decode");
   return SMER_OK;
 }

@@ -131,10 +131,16 @@ class DecodeSession:
         scale = 1.0 / math.sqrt(D)
         sstride = self.Tmax * 2 * d
         cstride = self.Smax * 2 * d
+        fused = dt == torch.bfloat16
         for li, L in enumerate(W.dec):
-            qkv = ops.linear(x, L.sa_w, L.sa_b)
             cache = self.self_kv[li]
-            ops.kv_scatter(qkv[:, d:], cache, req_t, pos_t, row_stride=2 * d, req_stride=sstride)
+            if fused:  # the QKV epilogue appends K/V to the cache (no scatter launch)
+                qkv = ops.linear_decode(x, L.sa_w, L.sa_b, kv=cache, kv_req=req_t, kv_pos=pos_t,
+                                        kv_row_stride=2 * d, kv_req_stride=sstride, kv_col0=d)
+            else:
+                qkv = ops.linear(x, L.sa_w, L.sa_b)
+                ops.kv_scatter(qkv[:, d:], cache, req_t, pos_t, row_stride=2 * d,
+                               req_stride=sstride)
             o = torch.empty(M, d, dtype=dt, device=dev)
             ops.attn_decode(qkv[:, :d], cache, cache.view(-1)[d:], req_t, nks_t, o, H=H, D=D,
                             row_stride=2 * d, req_stride=sstride, scale=scale)
@@ -170,11 +176,11 @@ class DecodeSession:
         torch.cuda.current_stream().wait_stream(s)
         self.graph = g
 
-    def step(self, feeds):
-        """feeds: list of (slot, new_token_ids (1 or 2), first_position).
-        Returns fp32 logits [len(feeds), V] (numpy) of each feed's LAST new
-        token.  Slots not fed this step are dummies."""
-        R, Tm = self.R, self.Tmax
+    def _load_feeds(self, feeds):
+        """Host-built step rows: feeds = [(slot, new_token_ids (1 or 2),
+        first_position)]; every other row is a dummy into the trash slot.
+        Returns the rows of each feed's last token."""
+        Tm = self.Tmax
         ids = self.ids_h.numpy()
         meta = self.meta_h.numpy()
         ids[:] = 0
@@ -199,6 +205,13 @@ class DecodeSession:
             last.append(2 * slot + 1)
         self.ids_t.copy_(self.ids_h, non_blocking=True)
         self.meta_t.copy_(self.meta_h, non_blocking=True)
+        return last
+
+    def step(self, feeds):
+        """feeds: list of (slot, new_token_ids (1 or 2), first_position).
+        Returns fp32 logits [len(feeds), V] (numpy) of each feed's LAST new
+        token.  Slots not fed this step are dummies."""
+        last = self._load_feeds(feeds)
         if self.use_graph:
             self._ensure_graph()
             self.graph.replay()
@@ -207,3 +220,95 @@ class DecodeSession:
         self.logits_h.copy_(self.logits_t, non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return self.logits_h.numpy()[last]
+
+    # ------------------------------------------------------------------
+    # greedy decode with the grammar on device (csrc/decode_ops.hip)
+    # ------------------------------------------------------------------
+    N_STATE = 12
+
+    def greedy_decode(self, spans, keep, cls, *, eos, m0, lookahead=3, max_span=100):
+        """Run the greedy infill loop of `spans` (generation._Span, one per
+        request slot 0..len-1, freshly started, sources prefilled) entirely
+        on device: each step is one replay of the captured decoder step +
+        grammar kernel; the host only polls the live count, `lookahead`
+        steps behind.  Returns (per-request emitted ids, steps, error flags);
+        the caller replays the ids through its host spans."""
+        R = len(spans)
+        if R > self.R:
+            raise ValueError("more spans than session slots")
+        dev = self.dev
+        nm = max(1, max(s.n_masks for s in spans))
+        cap = self.Tmax
+        st = np.zeros((self.R, self.N_STATE), dtype=np.int32)
+        tg = np.zeros((self.R, nm), dtype=np.int8)
+        from .generation import _target_code  # late import: generation imports decode
+        feeds = []
+        for r, sp in enumerate(spans):
+            st[r, 2] = 1                      # this_in = [m_0]
+            st[r, 4] = sp.n_masks
+            st[r, 5] = 1 if sp.done else 0
+            st[r, 6] = int(bool(sp.no_whole))
+            for k, t in enumerate(sp.mask_target[:nm]):
+                tg[r, k] = _target_code(t)
+            if not sp.done:
+                st[r, 0] = 1                  # m_0 is fed at position 0 below
+                feeds.append((r, [m0], 0))
+        st[R:, 5] = 1
+        if not feeds:
+            return [[] for _ in range(R)], 0, np.zeros(R, dtype=np.int32)
+        self.g_state = torch.from_numpy(st).to(dev)
+        self.g_targets = torch.from_numpy(tg).to(dev)
+        self.g_keep = torch.from_numpy(np.ascontiguousarray(keep, dtype=np.uint8)).to(dev)
+        self.g_cls = torch.from_numpy(np.ascontiguousarray(cls, dtype=np.uint8)).to(dev)
+        self.g_srclen = torch.from_numpy(self.src_len.astype(np.int32)).to(dev)
+        self.g_out = torch.zeros(self.R, cap, dtype=torch.int32, device=dev)
+        self.g_alive = torch.zeros(1, dtype=torch.int32, device=dev)
+        gargs = dict(eos=eos, m0=m0, trash_pos=self.Tmax - 1, max_span=max_span)
+
+        def grammar():
+            ops.grammar_greedy_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
+                                    self.g_cls, self.g_srclen, self.ids_t, self.meta_t, self.g_out,
+                                    self.g_alive, **gargs)
+
+        # warm the decoder step eagerly (dummy rows only), then capture
+        # step + grammar; the grammar kernel never runs outside the graph
+        self._load_feeds([])
+        self._run()
+        torch.cuda.synchronize()
+        gs = torch.cuda.Stream()
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs):
+                self._run()
+                grammar()
+        torch.cuda.current_stream().wait_stream(gs)
+        self._load_feeds(feeds)
+        max_steps = max([s.n_masks for s in spans] + [0]) * (max_span + 1) + 2
+        ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
+        rv = ring.numpy()
+        inflight = []
+        steps = None
+        issued = 0
+        while steps is None:
+            if len(inflight) > lookahead or (issued >= max_steps and inflight):
+                j, ev, slot = inflight.pop(0)
+                ev.synchronize()
+                if rv[slot] == 0:
+                    steps = j + 1
+                    break
+                continue
+            if issued >= max_steps:
+                raise RuntimeError("greedy_decode: no convergence within %d steps" % max_steps)
+            g.replay()
+            slot = issued % len(rv)
+            ring[slot:slot + 1].copy_(self.g_alive, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            inflight.append((issued, ev, slot))
+            issued += 1
+        torch.cuda.synchronize()
+        st = self.g_state.cpu().numpy()
+        out = self.g_out.cpu().numpy()
+        ids = [out[r, :min(int(st[r, 7]), cap)].tolist() for r in range(R)]
+        return ids, steps, st[:R, 8].copy()

@@ -139,6 +139,68 @@ def model_generate(model, src, tgt, device, return_weights=False):
 # --------------------------------------------------------------------------
 # the per-span grammar state machine (generation.py:528-687)
 # --------------------------------------------------------------------------
+N_GRAMMAR_STATES = 13
+
+
+def _target_code(tc):
+    """Control target of a mask: 'r' 0, 'd' 1, 'o' 2, 'p' 3, anything else
+    't' 4 (the reference's `else: is_tensile`, generation.py:575-583)."""
+    return {'r': 0, 'd': 1, 'o': 2, 'p': 3}.get(tc, 4)
+
+
+def grammar_spec(v, code):
+    """(sampling flags, redraw check, failure message) of grammar state
+    `code` (generation.py:549-630):
+    0 sep, 1 continue, 2/3 pitch, 4/5 rest (+no_whole), 6-9 first token of a
+    d/o/p/t control span, 10 first token of a note span, 11/12 free."""
+    if code == 0:
+        return (dict(no_rest=True, no_sep=True, no_eos=True, no_whole_duration=True,
+                     no_control=True),
+                lambda i: i in v.rest_indices or i == v.eos_index or
+                i == v.duration_only_indices[0], "in sep failed")
+    if code == 1:
+        return (dict(no_rest=True, no_sep=True, no_duration=True, no_continue=True,
+                     no_eos=True, no_control=True),
+                lambda i: i not in v.pitch_indices, 'in continue failed')
+    if code in (2, 3):
+        return (dict(no_rest=True, no_sep=True, no_continue=True,
+                     no_whole_duration=code == 3, no_eos=True, no_control=True),
+                lambda i: i not in v.duration_only_indices and i not in v.pitch_indices,
+                'in pitch failed')
+    if code in (4, 5):
+        return (dict(no_pitch=True, no_rest=True, no_sep=True, no_continue=True,
+                     no_whole_duration=code == 5, no_eos=True, no_control=True),
+                lambda i: i not in v.duration_only_indices, 'in rest failed')
+    if 6 <= code <= 9:
+        return {('is_density', 'is_occupation', 'is_polyphony', 'is_tensile')[code - 6]: True}, None, ''
+    if code == 10:
+        return (dict(no_duration=True, no_control=True),
+                lambda i: i in v.duration_only_indices, 'start failed')
+    return dict(no_whole_duration=code == 12, no_control=True), None, ''
+
+
+def grammar_tables(vocab, all_controls):
+    """Device tables of the greedy grammar kernel: keep uint8 [13, V]
+    (allowed_ids of every state) and token classes cls uint8 [V]
+    (1 continue, 2 pitch, 4 duration-only, 8 'sep', 16 'rest', 32 control)."""
+    V = vocab.vocab_size
+    keep = np.stack([allowed_ids(vocab, **grammar_spec(vocab, c)[0])
+                     for c in range(N_GRAMMAR_STATES)]).astype(np.uint8)
+    cls = np.zeros(V, dtype=np.uint8)
+    if getattr(vocab, "continue_index", None) is not None:
+        cls[vocab.continue_index] |= 1
+    cls[vocab.pitch_indices] |= 2
+    cls[vocab.duration_only_indices] |= 4
+    for i in range(V):
+        ch = vocab.index2char(i)
+        if ch == 'sep':
+            cls[i] |= 8
+        if ch == 'rest':
+            cls[i] |= 16
+    cls[[int(c) for c in all_controls]] |= 32
+    return keep, cls
+
+
 class _Span:
     """Decoding state of one request: mask index, span tokens, grammar flags."""
 
@@ -181,36 +243,27 @@ class _Span:
                 break
         return idx
 
+    def state_code(self):
+        """Grammar state of the current prefix (generation.py:549-630), the
+        code csrc/decode_ops.hip grammar_state() computes on device."""
+        nw = int(bool(self.no_whole))
+        if self.in_sep:
+            return 0
+        if self.in_continue:
+            return 1
+        if self.in_pitch:
+            return 2 + nw
+        if self.in_rest:
+            return 4 + nw
+        if len(self.this_in) == 1:
+            tc = _target_code(self.mask_target[self.mask_idx])
+            return 10 if tc == 0 else 5 + tc
+        return 11 + nw
+
     def spec(self):
         """(sampling flags, redraw check, failure message) of the current
         grammar state (generation.py:549-630)."""
-        v = self.v
-        if self.in_sep:
-            return (dict(no_rest=True, no_sep=True, no_eos=True, no_whole_duration=True,
-                         no_control=True),
-                    lambda i: i in v.rest_indices or i == v.eos_index or
-                    i == v.duration_only_indices[0], "in sep failed")
-        if self.in_continue:
-            return (dict(no_rest=True, no_sep=True, no_duration=True, no_continue=True,
-                         no_eos=True, no_control=True),
-                    lambda i: i not in v.pitch_indices, 'in continue failed')
-        if self.in_pitch:
-            return (dict(no_rest=True, no_sep=True, no_continue=True,
-                         no_whole_duration=self.no_whole, no_eos=True, no_control=True),
-                    lambda i: i not in v.duration_only_indices and i not in v.pitch_indices,
-                    'in pitch failed')
-        if self.in_rest:
-            return (dict(no_pitch=True, no_rest=True, no_sep=True, no_continue=True,
-                         no_whole_duration=self.no_whole, no_eos=True, no_control=True),
-                    lambda i: i not in v.duration_only_indices, 'in rest failed')
-        if len(self.this_in) == 1:
-            tc = self.mask_target[self.mask_idx]
-            if tc != 'r':
-                flag = {'d': 'is_density', 'o': 'is_occupation', 'p': 'is_polyphony'}.get(tc, 'is_tensile')
-                return {flag: True}, None, ''
-            return (dict(no_duration=True, no_control=True),
-                    lambda i: i in v.duration_only_indices, 'start failed')
-        return dict(no_whole_duration=self.no_whole, no_control=True), None, ''
+        return grammar_spec(self.v, self.state_code())
 
     def advance(self, logit):
         """Consume the logits of the current prefix's last position."""
@@ -305,10 +358,17 @@ infill = generation_all
 
 
 def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logger=None,
-                     max_tgt=None, precision=None, return_stats=False):
+                     max_tgt=None, precision=None, return_stats=False, device_grammar=True):
     """Decode many infill requests in lockstep on one KV-cached session.
 
     requests: list of (events, tracks_to_generate, bars_to_generate).
+    Greedy decoding runs the grammar on device (`device_grammar`, the
+    default): the step graph ends in the grammar kernel that picks every
+    request's token and writes the next step's feed, so steps replay back
+    to back; the emitted ids are then replayed through the host `_Span`s,
+    which rebuild exactly the reference's event lists (and log the
+    reference's redraw failures).  `device_grammar=False` (or sampling)
+    keeps the per-step host loop.
     Returns a list of (restored, mask_track_names, mask_bar_names) (None
     where nothing was masked), and optionally {'tokens', 'steps'}."""
     t0 = time.perf_counter()
@@ -327,6 +387,21 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         t2 = time.perf_counter()
         t_dev = 0.0
         fed = [0] * R
+        if greedy and device_grammar:
+            keep, cls = grammar_tables(vocab, all_controls)
+            m0 = vocab.char2index('m_0')
+            ts = time.perf_counter()
+            seqs, steps, err = sess.greedy_decode(spans, keep, cls, eos=vocab.eos_index, m0=m0)
+            t_dev = time.perf_counter() - ts
+            if np.any(err):
+                raise ValueError("decoder prefix exceeds session max_tgt %d" % (sess.Tmax - 1))
+            for sp, seq in zip(spans, seqs):
+                for idx in seq:
+                    _, chk, msg = sp.spec()
+                    sp.commit_greedy(idx, chk, msg)
+                if not sp.done:
+                    raise RuntimeError("device grammar and host replay disagree")
+                tokens += len(seq)
         while True:
             live = [i for i in range(R) if not spans[i].done]
             if not live:

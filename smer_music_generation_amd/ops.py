@@ -206,6 +206,40 @@ def kv_scatter(src, cache, row_req, row_pos, *, row_stride, req_stride):
          _p(cache), int(row_stride), int(req_stride), _p(row_req), _p(row_pos), _stream())
 
 
+def linear_decode(x, w, bias=None, *, relu=False, residual=None, out=None, out_f32=None, kv=None,
+                  kv_req=None, kv_pos=None, kv_row_stride=0, kv_req_stride=0, kv_col0=0):
+    """Decode-step Linear (bf16, M <= 256): out = x @ w^T + bias (+relu)
+    (+residual); output columns >= kv_col0 are also appended to the K/V
+    cache `kv` at (kv_req[m], kv_pos[m])."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None and out_f32 is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    call("smer_linear_decode", M, N, K, _p(x), _ld(x), _p(w), _ld(w), _p(bias), int(bool(relu)),
+         _p(residual), _ld(residual) if residual is not None else 0, _p(out),
+         _ld(out) if out is not None else 0, _p(out_f32), _ld(out_f32) if out_f32 is not None else 0,
+         _p(kv), int(kv_row_stride), int(kv_req_stride), _p(kv_req), _p(kv_pos), int(kv_col0),
+         _stream())
+    return out if out is not None else out_f32
+
+
+def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, out_tok, alive, *,
+                        eos, m0, trash_pos, max_span=100):
+    R, nst = state.shape
+    V = keep.shape[1]
+    for t, dt in ((state, torch.int32), (targets, torch.int8), (keep, torch.uint8),
+                  (cls, torch.uint8), (src_len, torch.int32), (ids, torch.int64),
+                  (meta, torch.int32), (out_tok, torch.int32), (alive, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise RuntimeError("grammar_greedy_step: expected contiguous %s" % dt)
+    if logits.shape[0] < 2 * R or ids.shape[0] != 2 * R or meta.shape != (4, 2 * R) or \
+            targets.shape[0] != R or keep.shape[0] != 13 or cls.shape[0] != V or src_len.shape[0] != R:
+        raise RuntimeError("grammar_greedy_step: shape mismatch")
+    call("smer_grammar_greedy_step", R, V, _p(logits), _ld(logits), _p(state), nst, _p(targets),
+         targets.shape[1], _p(keep), _p(cls), int(eos), int(m0), int(trash_pos), int(max_span),
+         _p(src_len), _p(ids), _p(meta), _p(out_tok), out_tok.shape[1], _p(alive), _stream())
+
+
 # ---------------------------------------------------------------------------
 def layernorm(x, gamma, beta, y, mean, rstd, eps=1e-5):
     M, N = x.shape

@@ -142,7 +142,8 @@ def test_gemm_identity_asymmetric():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N,K", [(192, 256, 128), (640, 264, 136), (40, 264, 136)])
+@pytest.mark.parametrize("M,N,K", [(192, 256, 128), (640, 264, 136), (40, 264, 136),
+                                   (64, 512, 2048), (130, 264, 1040)])
 def test_gemm_epilogue(dtype, M, N, K):
     """Skinny (M <= 256) and tiled kernels, incl. N and K tails."""
     O = ops()
@@ -326,17 +327,19 @@ def test_attention_weights(dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("D", [64, 32, 128, 24])
-def test_decode_attention(dtype, D):
-    """Vectorised online-softmax kernel (D = 32/64/128) and the generic
-    fallback (D = 24)."""
+@pytest.mark.parametrize("cap", [1000, 300])
+def test_decode_attention(dtype, D, cap):
+    """Vectorised online-softmax kernel (D = 32/64/128; 8-wave x 4-step
+    config for long caches, 4 x 2 for short) and the generic fallback
+    (D = 24)."""
     O = ops()
-    H, cap, R = 4, 1000, 3
+    H, R = 4, 3
     d = H * D
     kc = torch.randn(R, cap, d, device=dev).to(dtype)
     vc = torch.randn(R, cap, d, device=dev).to(dtype)
     q = torch.randn(5, d, device=dev).to(dtype)
     row_req = torch.tensor([0, 1, 1, 2, 2], dtype=torch.int32, device=dev)
-    nkeys = torch.tensor([1, 17, 18, 1000, 64], dtype=torch.int32, device=dev)
+    nkeys = torch.tensor([1, 17, 18, cap, 64], dtype=torch.int32, device=dev)
     out = torch.empty(5, d, device=dev, dtype=dtype)
     O.attn_decode(q, kc, vc, row_req, nkeys, out, H=H, D=D, row_stride=d, req_stride=cap * d,
                   scale=0.125)
@@ -351,10 +354,10 @@ def test_decode_attention(dtype, D):
     # scatter
     src = torch.randn(2, d, device=dev).to(dtype)
     O.kv_scatter(src, kc, torch.tensor([2, 0], dtype=torch.int32, device=dev),
-                 torch.tensor([5, 999], dtype=torch.int32, device=dev), row_stride=d,
+                 torch.tensor([5, cap - 1], dtype=torch.int32, device=dev), row_stride=d,
                  req_stride=cap * d)
     torch.cuda.synchronize()
-    assert torch.equal(kc[2, 5], src[0]) and torch.equal(kc[0, 999], src[1])
+    assert torch.equal(kc[2, 5], src[0]) and torch.equal(kc[0, cap - 1], src[1])
 
 
 # ------------------------------------------------------------ layernorm
@@ -505,3 +508,29 @@ def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
     sel = np.ones((Lq, Lk), bool) if not causal else np.tril(np.ones((Lq, Lk), bool))
     g = got[:, :Lq, :Lk].astype(bool)
     assert (g[:, sel] == ref[:, sel]).all()
+
+
+# ------------------------------------------------------------ decode linear
+@pytest.mark.parametrize("M,N,K", [(64, 1536, 512), (128, 512, 2048), (40, 264, 512),
+                                   (256, 264, 1024)])
+def test_linear_decode_kv_scatter(M, N, K):
+    """Decode Linear: bias, ReLU, residual, and the K/V scatter of the
+    output columns >= kv_col0 into a per-request cache."""
+    O = ops()
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device=dev).to(bf)
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(bf)
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(bf)
+    col0 = (N // 3) // 8 * 8
+    R = 5
+    T = M // R + 1
+    cache = torch.zeros(R, T, N - col0, device=dev, dtype=bf)
+    req = torch.arange(M, device=dev, dtype=torch.int32) % R
+    pos = torch.arange(M, device=dev, dtype=torch.int32) // R
+    out = O.linear_decode(x, w, b, relu=True, residual=res, kv=cache, kv_req=req, kv_pos=pos,
+                          kv_row_stride=N - col0, kv_req_stride=T * (N - col0), kv_col0=col0)
+    ref = torch.relu(x.float() @ w.float().t() + b) + res.float()
+    torch.cuda.synchronize()
+    assert rel_err(out, ref) < 2e-2
+    assert torch.equal(cache[req.long(), pos.long()], out[:, col0:])

@@ -120,3 +120,55 @@ def test_batched_greedy_commit_matches_per_row_sampling():
         assert ia == ib and a.prefix() == b.prefix()
         n += 1
     assert a.done and b.done and a.total == b.total
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_device_grammar_mirror_matches_host_spans(seed):
+    """The device greedy-grammar kernel's state machine (mirrored in
+    tests/grammar_mirror.py) emits the same ids and feeds the same prefix
+    tokens at the same positions as the host `_Span` loop."""
+    from tests import grammar_mirror as gm
+    from smer_music_generation_amd.generation import (_prepare, _Span, _target_code,
+                                                      grammar_tables)
+    from smer_music_generation_amd.synth import synth_events
+    v = WordVocab(0, ["key", "tensile", "density", "polyphony", "occupation"])
+    ac = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
+    keep, cls = grammar_tables(v, ac)
+    ev = synth_events(seed, n_bars=5, n_tracks=3)
+    prep = _prepare(list(ev), v, [seed % 3, (seed + 1) % 3], [1, 3])
+    sp = _Span(v, prep[0], prep[3], ac, prep[4], True, None)
+    m0 = v.char2index('m_0')
+    st = dict(pos=1, flags=0, len=1, midx=0, nmask=sp.n_masks, done=0,
+              no_whole=int(bool(sp.no_whole)), count=0, err=0)
+    tg = [_target_code(t) for t in sp.mask_target]
+    rng = np.random.default_rng(seed)
+    fed = [m0]  # tokens fed so far, by position
+    trash = 100 * sp.n_masks + 8
+    n = 0
+    while not sp.done:
+        assert sp.state_code() == gm.state_code(st["flags"], st["len"], tg[st["midx"]],
+                                                st["no_whole"])
+        lg = (rng.standard_normal(v.vocab_size) * 4).astype(np.float32)
+        lg[rng.integers(0, v.vocab_size, 3)] = lg.max()
+        if n % 9 == 8:
+            lg[v.eos_index] = lg.max() + 1.0
+        f, chk, msg = sp.spec()
+        ih = int(np.argmax(np.where(allowed_ids_cached(v, f), lg, np.float32(-100.0))))
+        sp.commit_greedy(ih, chk, msg)
+        idx, rows = gm.step(st, tg, keep, cls, lg, eos=v.eos_index, m0=m0, trash_pos=trash,
+                            src_len=len(prep[0]))
+        assert idx == ih
+        for tok, pos, nks, nkc in rows:
+            if pos == trash:
+                continue
+            assert pos == len(fed) and nks == pos + 1
+            fed.append(tok)
+        if not sp.done:
+            assert fed == sp.prefix()
+        n += 1
+    assert st["done"] == 1 and st["err"] == 0 and st["count"] == n
+
+
+def allowed_ids_cached(v, flags):
+    from smer_music_generation_amd.generation import allowed_ids
+    return allowed_ids(v, **flags)
