@@ -416,6 +416,26 @@ namespace {
 constexpr int G2 = 256, G2K = 64;
 constexpr int G2_OP = G2 * G2K * 2;     // 32 KiB per operand per stage
 constexpr int G2_STAGE = 2 * G2_OP;     // 64 KiB
+// epilogue X (residual / gate) slots: A beyond the two stages, B after the
+// fp32 staging rows (64 x (256 + 4) floats)
+constexpr int G2_XA = 2 * G2_STAGE;                 // 128 KiB
+constexpr int G2_XB = 64 * (G2 + 4) * 4;            // 65 KiB
+constexpr int G2_LDS = G2_XA + 64 * G2 * 2;         // 160 KiB total
+
+// 64 rows x 256 bf16 columns of X (row-major, ld) -> LDS [64][512 B], by
+// LDS-DMA: wave w's instruction c fills 1 KiB = rows 2(4w+c), +1.
+__device__ __forceinline__ void g2_xload(char* dst, const bf16* X, long ld, int r0, int c0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int chunk = wave * 4 + c;
+    const int row = chunk * 2 + (lane >> 5);
+    const bf16* src = X + (long)(r0 + row) * ld + c0 + (lane & 31) * 8;
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + chunk * 1024), 16, 0, 0);
+  }
+}
 
 // LDS image of one operand stage: KC (row image): row r at r*128 B, 16-B
 // chunks XOR (r & 7); column image: k-row at k*512 B, 8-B units XOR
@@ -462,7 +482,7 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int
 }
 }  // namespace
 
-template <bool AK, bool BKC>
+template <bool AK, bool BKC, bool FAST>
 __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int K,
                                                               const bf16* __restrict__ A, long lda,
                                                               const bf16* __restrict__ B, long ldb,
@@ -479,6 +499,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
   const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
   constexpr int GM = 4;
   const int nk = K / G2K;
+  // streamed-epilogue fast path: whole tiles, bf16 C only, at most one of
+  // residual / gate (the X operand DMA'd through LDS)
+  constexpr bool fast = FAST;  // host: gemm256_fast_ok
+  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);
+  const long ldx = e.residual ? e.ldr : e.ldg;
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;
@@ -494,10 +519,19 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (fast && e.bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8 + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
     g2_glds<AK>(smem, A, lda, M, m0, 0, tid);
     g2_glds<BKC>(smem + G2_OP, B, ldb, N, n0, 0, tid);
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // stage kt landed (vmcnt(0) + barrier); stage kt-1 fully read
+      // X rows of the first epilogue pass into slot A (beyond the stages)
+      if (fast && xsrc && kt == nk / 2) g2_xload(smem + G2_XA, xsrc, ldx, m0, n0, tid);
       if (kt + 1 < nk) {
         char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
         g2_glds<AK>(nb, A, lda, M, m0, (kt + 1) * G2K, tid);
@@ -520,10 +554,70 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
 
-    // epilogue: 4 passes of 64 rows x 256 columns (fp32 in LDS)
     const int g = lane >> 4, c16 = lane & 15;
     constexpr int EP_LD = G2 + 4;
     float* ep = reinterpret_cast<float*>(smem);
+    if constexpr (FAST) {
+      // Streamed epilogue: the residual / gate tile of pass p is DMA'd into
+      // LDS (slot A for even passes, B for odd) one pass ahead, so the
+      // passes no longer pay a dependent HBM round trip each; the bias is in
+      // registers (a thread always owns the same 8 columns).
+      if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid);
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+        if (wm == (pass >> 1)) {
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * (pass & 1) + ii;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+          }
+        }
+        __syncthreads();  // ep rows written; X(pass) landed; X(pass-1) slot free
+        if (xsrc && pass >= 1 && pass < 3)
+          g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
+        const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
+        const int ch = tid & 31;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int row = (tid >> 5) + 16 * c;
+          const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
+          float v[8];
+          const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+          const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + bv[k];
+          if (e.relu) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+          }
+          if (e.drop_thr)
+            smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
+          if (xsrc) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
+            if (e.residual) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] += (float)xv[k];
+            } else {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] = (float)xv[k] > 0.f ? v[k] * e.gate_scale : 0.f;
+            }
+          }
+          bf16x8 o;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+        }
+        __syncthreads();
+      }
+      continue;
+    }
+
+    // generic epilogue: 4 passes of 64 rows x 256 columns (fp32 in LDS)
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
       // rows [64*pass, 64*pass+64) belong to wm = pass >> 1, fragments
@@ -817,6 +911,16 @@ static int smer_num_cus() {
   return cache[dev];
 }
 
+// minimum K depth of a split-K slice (SMER_SPLITK_DEPTH overrides; A/B runs)
+static int smer_splitk_depth() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_SPLITK_DEPTH");
+    v = e ? std::max(64, atoi(e)) : 1024;
+  }
+  return v;
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -826,7 +930,7 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   // add slab traffic (split * M * N * 8 bytes through HBM)
   // (floor: a partial second wave of workgroups costs a whole slice time)
   long s = (2L * smer_num_cus()) / tiles;
-  s = std::min<long>(s, K / 1024);
+  s = std::min<long>(s, K / smer_splitk_depth());
   // slabs of M*N floats plus M floats of row-sum partials per K slice
   s = std::min<long>(s, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
   s = std::max<long>(1, std::min<long>(s, 64));
@@ -855,11 +959,18 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
       static bool attr_set = false;  // > 64 KiB dynamic LDS must be opted into
       if (!attr_set) {
-        hipFuncSetAttribute((const void*)gemm256_bf16_kernel<AK, BKC>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G2_STAGE);
+        hipFuncSetAttribute((const void*)gemm256_bf16_kernel<AK, BKC, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+        hipFuncSetAttribute((const void*)gemm256_bf16_kernel<AK, BKC, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
         attr_set = true;
       }
-      hipLaunchKernelGGL((gemm256_bf16_kernel<AK, BKC>), dim3(grid), dim3(512), 2 * G2_STAGE, s,
+      // streamed-epilogue variant: whole tiles, bf16 C only, at most one of
+      // residual / gate
+      const bool fast = e.vec && e.C && !e.Cf && !e.kv && M % G2 == 0 && N % G2 == 0 &&
+                        !(e.residual && e.gate);
+      auto kern = fast ? gemm256_bf16_kernel<AK, BKC, true> : gemm256_bf16_kernel<AK, BKC, false>;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), G2_LDS, s,
                          M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
       return;
     }

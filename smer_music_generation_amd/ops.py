@@ -60,9 +60,19 @@ class KernelTimer:
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e, _ in self.records]
-        fl = [f for _, _, f in self.records]
+        ms = [r[0].elapsed_time(r[1]) for r in self.records]
+        fl = [r[2] for r in self.records]
         return {"launches": len(ms), "total_ms": float(sum(ms)), "flops": float(sum(fl))}
+
+    def by_shape(self):
+        """{tag: (launches, total_ms, flops)} over the recorded launches."""
+        torch.cuda.synchronize()
+        out = {}
+        for r in self.records:
+            tag = r[3] if len(r) > 3 else "?"
+            n, t, f = out.get(tag, (0, 0.0, 0.0))
+            out[tag] = (n + 1, t + r[0].elapsed_time(r[1]), f + r[2])
+        return out
 
 
 GEMM_TIMER = None  # set to a KernelTimer to instrument smer_gemm launches
@@ -82,7 +92,12 @@ def gemm(A, B, *, M, N, K, a_kcontig=True, b_kcontig=True, out=None, out_f32=Non
                relu, residual, gate, gate_scale, drop_p, seed)
     if timer is not None:
         ev1.record()
-        timer.records.append((ev0, ev1, 2.0 * M * N * K))
+        epi = "".join(c for c, on in (("b", bias is not None), ("r", relu), ("d", drop_p > 0),
+                                      ("R", residual is not None), ("g", gate is not None),
+                                      ("f", out_f32 is not None), ("+", accumulate)) if on)
+        tag = "%s%s M%d N%d K%d %s" % ("n" if a_kcontig else "t", "t" if b_kcontig else "n",
+                                        M, N, K, epi)
+        timer.records.append((ev0, ev1, 2.0 * M * N * K, tag))
 
 
 _SPLITK_WS = {}
@@ -155,7 +170,8 @@ def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None):
              _stream())
         if timer is not None:
             ev1.record()
-            timer.records.append((ev0, ev1, 2.0 * Mo * x.shape[1] * T))
+            timer.records.append((ev0, ev1, 2.0 * Mo * x.shape[1] * T,
+                                  "wgrad+bias M%d N%d K%d" % (Mo, x.shape[1], T)))
         return
     gemm(dy, x, M=Mo, N=x.shape[1], K=T, a_kcontig=False, b_kcontig=False, out_f32=dw,
          accumulate=accumulate, dtype=dy.dtype)

@@ -130,6 +130,26 @@ def test_gemm256_large_m(M, N, K, bk):
     assert rel_err(Cf, base) < 2e-3
 
 
+@pytest.mark.parametrize("M,N,K,bk", [(8192, 2048, 512, False), (16384, 512, 1536, True)])
+def test_gemm256_streamed_epilogue_gate(M, N, K, bk):
+    """The 256x256 kernel's streamed epilogue with a ReLU-grad gate (the
+    dgrad into the FFN hidden layer) and with a bare residual."""
+    O = ops()
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    Wm = W if bk else W.t().contiguous()
+    G = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, gate=G, gate_scale=1.5)
+    base = A.float() @ W.float().t()
+    ref = torch.where(G.float() > 0, base * 1.5, torch.zeros_like(base))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 2e-2
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, residual=G)
+    torch.cuda.synchronize()
+    assert rel_err(C, base + G.float()) < 2e-2
+
+
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128
