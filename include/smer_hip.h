@@ -22,6 +22,8 @@
  *   smer_attn_decode     KV-cached single-step attention for the infill loop
  *                        (replaces the full recompute of generation.py:217)
  *   smer_kv_scatter      append new K/V rows to a per-request cache
+ *   smer_kv_scatter_heads  the cross-attention memory K/V (transformer.py:463)
+ *                        into a head-major per-request cache at prefill
  *   smer_linear_decode   decode-step Linear (M <= 256 rows) whose epilogue
  *                        also appends the new K/V columns to the cache
  *                        (transformer.py:459 per generated token)
@@ -125,11 +127,19 @@ int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
                       smer_stream_t stream);
 /* Decode attention: row r (query q[r], head h at column h*D) attends keys
  * 0..row_nkeys[r]-1 of request row_req[r] in caches laid out
- * cache[req * req_stride + j * row_stride + h*D + d]. */
+ * cache[req * req_stride + h * head_stride + j * row_stride + d]
+ * (head_stride <= 0 means D: heads side by side within a key row). */
 int smer_attn_decode(int dtype, int n_rows, int H, int D, const void* q, long ldq,
                      const void* kcache, const void* vcache, long row_stride, long req_stride,
-                     const int32_t* row_req, const int32_t* row_nkeys, void* o, long ldo,
-                     float scale, smer_stream_t stream);
+                     long head_stride, const int32_t* row_req, const int32_t* row_nkeys,
+                     void* o, long ldo, float scale, smer_stream_t stream);
+/* Head-major K/V fill: row m of src = [K heads | V heads] (2*H*D columns);
+ * (kv, h, dd) -> cache[row_req[m]*req_stride + kv*kv_stride + h*head_stride
+ * + row_pos[m]*D + dd] (the decode cross-attention memory, written once per
+ * request at prefill). */
+int smer_kv_scatter_heads(int dtype, int n_rows, int H, int D, const void* src, long lds,
+                          void* cache, long req_stride, long kv_stride, long head_stride,
+                          const int32_t* row_req, const int32_t* row_pos, smer_stream_t stream);
 int smer_kv_scatter(int dtype, int n_rows, int width, const void* src, long lds,
                     void* cache, long row_stride, long req_stride,
                     const int32_t* row_req, const int32_t* row_pos, smer_stream_t stream);

@@ -899,6 +899,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(int H, int D, const T*
                                                           long ldq, const T* __restrict__ kc,
                                                           const T* __restrict__ vc,
                                                           long row_stride, long req_stride,
+                                                          long head_stride,
                                                           const int32_t* __restrict__ row_req,
                                                           const int32_t* __restrict__ row_nkeys,
                                                           T* __restrict__ o, long ldo,
@@ -909,7 +910,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(int H, int D, const T*
   __shared__ float part[4][256];
   const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
   const int nk = row_nkeys[r];
-  const long base = (long)row_req[r] * req_stride + h * D;
+  const long base = (long)row_req[r] * req_stride + h * head_stride;
   for (int d = tid; d < D; d += 256) qs[d] = to_f32(q[(long)r * ldq + h * D + d]) * scale;
   __syncthreads();
   float mx = -INFINITY;
@@ -978,17 +979,17 @@ __device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) 
 template <typename T, int LPK, int UNR, int NW>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
-    long row_stride, long req_stride, const int32_t* __restrict__ row_req,
+    long row_stride, long req_stride, long head_stride, const int32_t* __restrict__ row_req,
     const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int GPW = 64 / LPK;  // key groups per wave
   constexpr int KPB = NW * GPW;  // keys per block step
   __shared__ float red_m[NW][LPK], red_l[NW][LPK], red_a[NW][LPK][VEC];
-  const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int h = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;  // heads of a row dispatch together
   const int lane = tid & 63, wave = tid >> 6;
   const int sub = lane % LPK, grp = wave * GPW + lane / LPK;
   const int nk = row_nkeys[r];
-  const long base = (long)row_req[r] * req_stride + h * (LPK * VEC) + sub * VEC;
+  const long base = (long)row_req[r] * req_stride + h * head_stride + sub * VEC;
   float qv[VEC];
   load16b<T>(q + (long)r * ldq + h * (LPK * VEC) + sub * VEC, qv);
 #pragma unroll
@@ -1002,8 +1003,16 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     for (int u = 0; u < UNR; ++u) {
       const int j = j0 + u * KPB + grp;
       const long off = base + (long)(j < nk ? j : 0) * row_stride;
-      kr[u] = *reinterpret_cast<const uint4*>(kc + off);
-      vr[u] = *reinterpret_cast<const uint4*>(vc + off);
+      if constexpr (NW == 8) {  // long memories: once-read per step, stream non-temporally
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(kc + off));
+        const u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vc + off));
+        kr[u] = make_uint4(a.x, a.y, a.z, a.w);
+        vr[u] = make_uint4(b.x, b.y, b.z, b.w);
+      } else {
+        kr[u] = *reinterpret_cast<const uint4*>(kc + off);
+        vr[u] = *reinterpret_cast<const uint4*>(vc + off);
+      }
     }
     float sc[UNR];
     float mx = m;
@@ -1091,6 +1100,27 @@ __global__ void kv_scatter_kernel(int n_rows, int width, const T* __restrict__ s
   if (idx >= (long)n_rows * width) return;
   int r = idx / width, c = idx % width;
   cache[(long)row_req[r] * req_stride + (long)row_pos[r] * row_stride + c] = src[(long)r * lds + c];
+}
+
+// Head-major K/V cache fill (decode cross-attention memory): src row m holds
+// [K heads | V heads] (2*H*D columns); element (kv, h, dd) of row m goes to
+// cache[req[m]*req_stride + kv*kv_stride + h*head_stride + pos[m]*D + dd],
+// so each (request, head) reads one contiguous key run per step.
+template <typename T>
+__global__ void kv_scatter_heads_kernel(int n_rows, int H, int D, const T* __restrict__ src,
+                                        long lds, T* __restrict__ cache, long req_stride,
+                                        long kv_stride, long head_stride,
+                                        const int32_t* __restrict__ row_req,
+                                        const int32_t* __restrict__ row_pos) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int cpr = 2 * H * D / VEC;  // 16-B chunks per row
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)n_rows * cpr) return;
+  const int m = idx / cpr, col = (idx % cpr) * VEC;
+  const int kv = col / (H * D), h = (col % (H * D)) / D, dd = col % D;
+  *reinterpret_cast<uint4*>(cache + (long)row_req[m] * req_stride + kv * kv_stride +
+                            h * head_stride + (long)row_pos[m] * D + dd) =
+      *reinterpret_cast<const uint4*>(src + (long)m * lds + col);
 }
 
 // ---------------------------------------------------------------------------
@@ -1264,34 +1294,36 @@ extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
 
 extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void* q, long ldq,
                                 const void* kcache, const void* vcache, long row_stride,
-                                long req_stride, const int32_t* row_req,
+                                long req_stride, long head_stride, const int32_t* row_req,
                                 const int32_t* row_nkeys, void* o, long ldo, float scale,
                                 smer_stream_t stream) {
   SMER_REQUIRE(D <= 256, "smer_attn_decode: head dim <= 256");
   if (n_rows == 0) return SMER_OK;
+  if (head_stride <= 0) head_stride = D;  // heads side by side within a key row
   {
     // vectorised path: 16-B aligned rows, LPK = D / (16 / elem) in {4, 8, 16}
     const int es = dtype == SMER_BF16 ? 2 : 4, vec = 16 / es;
     auto al = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
     const bool ok = (dtype == SMER_BF16 || dtype == SMER_F32) && D % vec == 0 && al(q) &&
                     al(kcache) && al(vcache) && al(o) && ldq % vec == 0 && ldo % vec == 0 &&
-                    row_stride % vec == 0 && req_stride % vec == 0;
+                    row_stride % vec == 0 && req_stride % vec == 0 && head_stride % vec == 0;
     const int lpk = D / vec;
     hipStream_t s = (hipStream_t)stream;
-    dim3 grid(n_rows, H);
+    dim3 grid(H, n_rows);  // the H blocks of a row read the same K/V rows together
     // key capacity of a request (cache rows): long memories get 8 waves x
     // 4 steps of loads in flight per block, short self-attention caches 4 x 2
-    const long cap_rows = req_stride / (row_stride > 0 ? row_stride : 1);
+    const long cap_rows = head_stride != D ? head_stride / (row_stride > 0 ? row_stride : 1)
+                                           : req_stride / (row_stride > 0 ? row_stride : 1);
     const bool big = cap_rows >= 512;
 #define SMER_DEC_VEC(T, L)                                                                        \
   if (big)                                                                                        \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8>), grid, dim3(512), 0, s, (const T*)q,  \
-                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,   \
-                       row_nkeys, (T*)o, ldo, scale);                                             \
+                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride,            \
+                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale);                       \
   else                                                                                            \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 2, 4>), grid, dim3(256), 0, s, (const T*)q,  \
-                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride, row_req,   \
-                       row_nkeys, (T*)o, ldo, scale)
+                       ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride,            \
+                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale)
     if (ok && (lpk == 4 || lpk == 8 || lpk == 16)) {
       if (dtype == SMER_BF16) {
         if (lpk == 4) SMER_DEC_VEC(bf16, 4); else if (lpk == 8) SMER_DEC_VEC(bf16, 8); else SMER_DEC_VEC(bf16, 16);
@@ -1304,19 +1336,19 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
     }
   }
   // key capacity bounded by req_stride / row_stride rows
-  long cap = req_stride / (row_stride > 0 ? row_stride : 1);
+  long cap = (head_stride != D ? head_stride : req_stride) / (row_stride > 0 ? row_stride : 1);
   SMER_REQUIRE(cap > 0 && cap * 4 <= 150 * 1024, "smer_attn_decode: cache capacity too large");
   hipStream_t s = (hipStream_t)stream;
   size_t shm = (size_t)cap * sizeof(float);
   dim3 grid(n_rows, H);
   if (dtype == SMER_BF16)
     hipLaunchKernelGGL(attn_decode_kernel<bf16>, grid, dim3(256), shm, s, H, D, (const bf16*)q, ldq,
-                       (const bf16*)kcache, (const bf16*)vcache, row_stride, req_stride, row_req,
-                       row_nkeys, (bf16*)o, ldo, scale);
+                       (const bf16*)kcache, (const bf16*)vcache, row_stride, req_stride,
+                       head_stride, row_req, row_nkeys, (bf16*)o, ldo, scale);
   else if (dtype == SMER_F32)
     hipLaunchKernelGGL(attn_decode_kernel<float>, grid, dim3(256), shm, s, H, D, (const float*)q,
                        ldq, (const float*)kcache, (const float*)vcache, row_stride, req_stride,
-                       row_req, row_nkeys, (float*)o, ldo, scale);
+                       head_stride, row_req, row_nkeys, (float*)o, ldo, scale);
   else
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_decode: dtype");
   SMER_CHECK_LAUNCH("smer_attn_decode");
@@ -1341,5 +1373,30 @@ extern "C" int smer_kv_scatter(int dtype, int n_rows, int width, const void* src
   else
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_kv_scatter: dtype");
   SMER_CHECK_LAUNCH("smer_kv_scatter");
+  return SMER_OK;
+}
+
+extern "C" int smer_kv_scatter_heads(int dtype, int n_rows, int H, int D, const void* src, long lds,
+                                     void* cache, long req_stride, long kv_stride,
+                                     long head_stride, const int32_t* row_req,
+                                     const int32_t* row_pos, smer_stream_t stream) {
+  const int es = dtype == SMER_BF16 ? 2 : 4, vec = 16 / es;
+  SMER_REQUIRE(dtype == SMER_BF16 || dtype == SMER_F32, "smer_kv_scatter_heads: dtype");
+  SMER_REQUIRE(n_rows >= 0 && H > 0 && D % vec == 0 && lds % vec == 0 && req_stride % vec == 0 &&
+                   kv_stride % vec == 0 && head_stride % vec == 0 && al16(src) && al16(cache),
+               "smer_kv_scatter_heads: 16-B vector layout required");
+  const long tot = (long)n_rows * (2 * H * D / vec);
+  if (tot == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((tot + 255) / 256));
+  if (dtype == SMER_BF16)
+    hipLaunchKernelGGL(kv_scatter_heads_kernel<bf16>, grid, dim3(256), 0, s, n_rows, H, D,
+                       (const bf16*)src, lds, (bf16*)cache, req_stride, kv_stride, head_stride,
+                       row_req, row_pos);
+  else
+    hipLaunchKernelGGL(kv_scatter_heads_kernel<float>, grid, dim3(256), 0, s, n_rows, H, D,
+                       (const float*)src, lds, (float*)cache, req_stride, kv_stride, head_stride,
+                       row_req, row_pos);
+  SMER_CHECK_LAUNCH("smer_kv_scatter_heads");
   return SMER_OK;
 }

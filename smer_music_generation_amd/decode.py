@@ -51,7 +51,10 @@ class DecodeSession:
             model.pos_enc.extend(max(self.Smax, self.Tmax))
         self.self_kv = [torch.zeros(self.R, self.Tmax, 2 * d, dtype=self.dt, device=dev)
                         for _ in range(eng.n_dec)]
-        self.cross_kv = [torch.zeros(self.R, self.Smax, 2 * d, dtype=self.dt, device=dev)
+        # cross-attention memory, head-major [R, K|V, H, Smax, D]: each
+        # (request, head) streams one contiguous key run per decode step
+        H, D = eng.H, eng.D
+        self.cross_kv = [torch.zeros(self.R, 2, H, self.Smax, D, dtype=self.dt, device=dev)
                          for _ in range(eng.n_dec)]
         self.src_len = np.zeros(self.R, dtype=np.int64)
         self.W = eng.weights(self.dt)
@@ -113,8 +116,9 @@ class DecodeSession:
         pos_t = torch.from_numpy(pos).to(dev)
         for li, L in enumerate(W.dec):
             kvc = ops.linear(mem, L.ckv_w, L.ckv_b)
-            ops.kv_scatter(kvc, self.cross_kv[li], req_t, pos_t, row_stride=2 * d,
-                           req_stride=self.Smax * 2 * d)
+            ops.kv_scatter_heads(kvc, self.cross_kv[li], req_t, pos_t, H=H, D=D,
+                                 req_stride=2 * H * self.Smax * D, kv_stride=H * self.Smax * D,
+                                 head_stride=self.Smax * D)
         for b, s in enumerate(slots):
             self.src_len[s] = lens[b]
 
@@ -130,7 +134,7 @@ class DecodeSession:
         ops.embed(self.ids_t, W.emb, pe2, x, positions=pos_t, scale=math.sqrt(d))
         scale = 1.0 / math.sqrt(D)
         sstride = self.Tmax * 2 * d
-        cstride = self.Smax * 2 * d
+        cstride = 2 * H * self.Smax * D
         fused = dt == torch.bfloat16
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
@@ -149,8 +153,9 @@ class DecodeSession:
             qc = ops.linear(x1, L.cq_w, L.cq_b)
             cc = self.cross_kv[li]
             oc = torch.empty(M, d, dtype=dt, device=dev)
-            ops.attn_decode(qc, cc, cc.view(-1)[d:], req_t, nkc_t, oc, H=H, D=D,
-                            row_stride=2 * d, req_stride=cstride, scale=scale)
+            ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
+                            row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
+                            scale=scale)
             y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
             x2, _, _ = eng._ln(y2, L.n2, dt)
             h = ops.linear(x2, L.l1_w, L.l1_b, relu=True)
@@ -255,7 +260,7 @@ class DecodeSession:
                 feeds.append((r, [m0], 0))
         st[R:, 5] = 1
         if not feeds:
-            return [[] for _ in range(R)], 0, np.zeros(R, dtype=np.int32)
+            return [[] for _ in range(R)], 0, np.zeros(R, dtype=np.int32), []
         self.g_state = torch.from_numpy(st).to(dev)
         self.g_targets = torch.from_numpy(tg).to(dev)
         self.g_keep = torch.from_numpy(np.ascontiguousarray(keep, dtype=np.uint8)).to(dev)
@@ -288,8 +293,11 @@ class DecodeSession:
         ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
         rv = ring.numpy()
         inflight = []
+        events = []
         steps = None
         issued = 0
+        ev_start = torch.cuda.Event(enable_timing=True)
+        ev_start.record()
         while steps is None:
             if len(inflight) > lookahead or (issued >= max_steps and inflight):
                 j, ev, slot = inflight.pop(0)
@@ -303,12 +311,14 @@ class DecodeSession:
             g.replay()
             slot = issued % len(rv)
             ring[slot:slot + 1].copy_(self.g_alive, non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=True)
             ev.record()
+            events.append(ev)
             inflight.append((issued, ev, slot))
             issued += 1
         torch.cuda.synchronize()
         st = self.g_state.cpu().numpy()
         out = self.g_out.cpu().numpy()
         ids = [out[r, :min(int(st[r, 7]), cap)].tolist() for r in range(R)]
-        return ids, steps, st[:R, 8].copy()
+        step_ms = [ev_start.elapsed_time(e) for e in events[:steps]]
+        return ids, steps, st[:R, 8].copy(), step_ms

@@ -148,7 +148,22 @@ def _target_code(tc):
     return {'r': 0, 'd': 1, 'o': 2, 'p': 3}.get(tc, 4)
 
 
+_SPEC_CACHE = {}
+
+
 def grammar_spec(v, code):
+    """(sampling flags, redraw check, failure message) of grammar state
+    `code`, built once per (vocab, code) (the per-token host replay of the
+    device decode calls this for every emitted id)."""
+    key = (id(v), code)
+    hit = _SPEC_CACHE.get(key)
+    if hit is None or hit[0] is not v:
+        hit = (v, _grammar_spec(v, code))
+        _SPEC_CACHE[key] = hit
+    return hit[1]
+
+
+def _grammar_spec(v, code):
     """(sampling flags, redraw check, failure message) of grammar state
     `code` (generation.py:549-630):
     0 sep, 1 continue, 2/3 pitch, 4/5 rest (+no_whole), 6-9 first token of a
@@ -214,6 +229,8 @@ class _Span:
         self.logger = logger
         self.m0 = vocab.char2index('m_0')
         self.eos = vocab.char2index('<eos>')
+        self._pitch = frozenset(vocab.pitch_indices)
+        self._dur = frozenset(vocab.duration_only_indices)
         self.n_masks = int(np.sum(np.asarray(src) == self.m0))
         self.mask_idx = 0
         self.tgt_inp = []
@@ -273,7 +290,7 @@ class _Span:
     def commit_greedy(self, idx, check, failmsg):
         """Greedy draw already taken (argmax over the masked logits): the
         reference's redraw loop would re-draw the same id 11 times."""
-        if check is not None and check(int(idx)) and self.logger is not None:
+        if self.logger is not None and check is not None and check(int(idx)):
             self.logger.info(failmsg)
         return self.commit(idx)
 
@@ -283,9 +300,9 @@ class _Span:
         ev = v.index2char(idx)
         if idx == v.continue_index:
             self.in_continue, self.in_sep = True, False
-        if idx in v.pitch_indices:
+        if idx in self._pitch:
             self.in_pitch, self.in_sep, self.in_continue = True, False, False
-        if idx in v.duration_only_indices:
+        if idx in self._dur:
             self.in_rest, self.in_pitch = False, False
         if ev == 'sep':
             self.in_sep = True
@@ -387,12 +404,17 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         t2 = time.perf_counter()
         t_dev = 0.0
         fed = [0] * R
+        latency = None
         if greedy and device_grammar:
             keep, cls = grammar_tables(vocab, all_controls)
             m0 = vocab.char2index('m_0')
             ts = time.perf_counter()
-            seqs, steps, err = sess.greedy_decode(spans, keep, cls, eos=vocab.eos_index, m0=m0)
+            seqs, steps, err, step_ms = sess.greedy_decode(spans, keep, cls, eos=vocab.eos_index,
+                                                           m0=m0)
             t_dev = time.perf_counter() - ts
+            # completion time of each request from the call's start: host
+            # preparation + prefill, then the GPU end time of its last step
+            latency = [(ts - t0) + (step_ms[len(q) - 1] / 1000.0 if q else 0.0) for q in seqs]
             if np.any(err):
                 raise ValueError("decoder prefix exceeds session max_tgt %d" % (sess.Tmax - 1))
             for sp, seq in zip(spans, seqs):
@@ -437,5 +459,6 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     if return_stats:
         t3 = time.perf_counter()
         return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,
-                     "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev}
+                     "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev,
+                     "request_latency_s": latency}
     return out

@@ -211,10 +211,19 @@ def attn_weights(q, k, lse, out, *, B, H, Lq, Lk, D, kpm=None, causal=False, sca
 
 
 def attn_decode(q, kcache, vcache, row_req, row_nkeys, out, *, H, D, row_stride, req_stride,
-                scale):
+                scale, head_stride=0):
     call("smer_attn_decode", dtype_code(q.dtype), q.shape[0], H, D, _p(q), _ld(q), _p(kcache),
-         _p(vcache), int(row_stride), int(req_stride), _p(row_req), _p(row_nkeys), _p(out),
-         _ld(out), float(scale), _stream())
+         _p(vcache), int(row_stride), int(req_stride), int(head_stride), _p(row_req),
+         _p(row_nkeys), _p(out), _ld(out), float(scale), _stream())
+
+
+def kv_scatter_heads(src, cache, row_req, row_pos, *, H, D, req_stride, kv_stride, head_stride):
+    """Rows of [K heads | V heads] into a head-major cache (see smer_hip.h)."""
+    if src.shape[1] != 2 * H * D:
+        raise RuntimeError("kv_scatter_heads: src must have 2*H*D columns")
+    call("smer_kv_scatter_heads", dtype_code(src.dtype), src.shape[0], H, D, _p(src), _ld(src),
+         _p(cache), int(req_stride), int(kv_stride), int(head_stride), _p(row_req), _p(row_pos),
+         _stream())
 
 
 def kv_scatter(src, cache, row_req, row_pos, *, row_stride, req_stride):

@@ -371,6 +371,26 @@ def test_decode_attention(dtype, D, cap):
         vh = vc[r, :n].float().view(n, H, D).transpose(0, 1)
         ref = (torch.softmax(qh @ kh.transpose(-1, -2) * 0.125, -1) @ vh).reshape(d)
         assert rel_err(out[i], ref) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
+    # head-major layout [R][H][cap][D] (the decode cross-attention memory),
+    # filled by kv_scatter_heads from [K heads | V heads] rows
+    kvh = torch.zeros(R, 2, H, cap, D, device=dev, dtype=dtype)
+    rows = torch.cat([kc.view(R * cap, d), vc.view(R * cap, d)], 1).contiguous()
+    rr = torch.arange(R * cap, device=dev, dtype=torch.int32) // cap
+    pp = torch.arange(R * cap, device=dev, dtype=torch.int32) % cap
+    if D % (8 if dtype == torch.bfloat16 else 4) == 0:
+        O.kv_scatter_heads(rows, kvh, rr, pp, H=H, D=D, req_stride=2 * H * cap * D,
+                           kv_stride=H * cap * D, head_stride=cap * D)
+        torch.cuda.synchronize()
+        assert torch.equal(kvh[:, 0].permute(0, 2, 1, 3).reshape(R, cap, d), kc)
+        assert torch.equal(kvh[:, 1].permute(0, 2, 1, 3).reshape(R, cap, d), vc)
+    else:
+        kvh[:, 0] = kc.view(R, cap, H, D).permute(0, 2, 1, 3)
+        kvh[:, 1] = vc.view(R, cap, H, D).permute(0, 2, 1, 3)
+    out2 = torch.empty_like(out)
+    O.attn_decode(q, kvh, kvh.view(-1)[H * cap * D:], row_req, nkeys, out2, H=H, D=D, row_stride=D,
+                  req_stride=2 * H * cap * D, head_stride=cap * D, scale=0.125)
+    torch.cuda.synchronize()
+    assert torch.equal(out2, out)
     # scatter
     src = torch.randn(2, d, device=dev).to(dtype)
     O.kv_scatter(src, kc, torch.tensor([2, 0], dtype=torch.int32, device=dev),

@@ -71,15 +71,22 @@ def main():
     print("%-34s %8.2f us" % ("layernorm M x 512", graph_time(lambda: ops.layernorm(x, g_, b_, y, mu, rs))))
     H, D = 8, 64
     for name, nk, cap in (("self nk=100", 100, 600), ("cross nk=%d" % S, S, S)):
-        cache = torch.randn(R, cap, 2 * d, device=dev).to(bf)
         req = (torch.arange(M, device=dev, dtype=torch.int32) // 2)
         nks = torch.full((M,), nk, device=dev, dtype=torch.int32)
         nks[0::2] = 1
         q = torch.randn(M, d, device=dev).to(bf)
         o = torch.empty(M, d, device=dev, dtype=bf)
-        t = graph_time(lambda: ops.attn_decode(q, cache, cache.view(-1)[d:], req, nks, o, H=H, D=D,
-                                               row_stride=2 * d, req_stride=cap * 2 * d,
-                                               scale=1 / math.sqrt(D)))
+        if name.startswith("self"):
+            cache = torch.randn(R, cap, 2 * d, device=dev).to(bf)
+            t = graph_time(lambda: ops.attn_decode(q, cache, cache.view(-1)[d:], req, nks, o, H=H,
+                                                   D=D, row_stride=2 * d, req_stride=cap * 2 * d,
+                                                   scale=1 / math.sqrt(D)))
+        else:  # head-major memory, as DecodeSession stores it
+            cache = torch.randn(R, 2, H, cap, D, device=dev).to(bf)
+            t = graph_time(lambda: ops.attn_decode(q, cache, cache.view(-1)[H * cap * D:], req, nks,
+                                                   o, H=H, D=D, row_stride=D,
+                                                   req_stride=2 * H * cap * D,
+                                                   head_stride=cap * D, scale=1 / math.sqrt(D)))
         byt = R * nk * 2 * d * 2
         print("%-34s %8.2f us  %7.1f GB/s" % ("attn_decode " + name, t, byt / t / 1e3))
     cache = torch.zeros(R, 600, 2 * d, device=dev).to(bf)
