@@ -210,11 +210,16 @@ def _pmc_traffic():
     if not files:
         return None
     s = json.load(open(files[-1]))
-    g = [v for k, v in s.items() if k.startswith("gemm_bf16_kernel")]
+    # the smer_gemm family: 128x128 and 256x256 tile kernels, skinny kernel,
+    # split-K slab reduction (one smer_gemm call = tile kernel [+ reduce])
+    g = [v for k, v in s.items() if k.startswith(("gemm_bf16_kernel", "gemm256_bf16_kernel",
+                                                    "gemm_skinny_bf16_kernel"))]
     n = sum(v["launches"] for v in g)
     if not n:
         return None
-    return {"bytes_per_launch": round(sum(v["hbm_bytes"] * v["launches"] for v in g) / n),
+    red = [v for k, v in s.items() if k.startswith("splitk_reduce_kernel")]
+    tot = sum(v["hbm_bytes"] * v["launches"] for v in g + red)
+    return {"bytes_per_launch": round(tot / n),
             "source": os.path.basename(files[-1])}
 
 

@@ -46,12 +46,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
   if (row >= M) return;
   const int nch = N >> 3;
   float v[LN_MAXC][8];
+  float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, loaded with x
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < LN_MAXC; ++c) {
     int ch = lane + 64 * c;
     if (ch < nch) {
       Vec8<T>::load(x + (long)row * ldx + ch * 8, v[c]);
+      Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
+      Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
 #pragma unroll
       for (int i = 0; i < 8; ++i) s += v[c][i];
     }
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
     if (ch < nch) {
       float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * rs * gamma[ch * 8 + i] + beta[ch * 8 + i];
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * rs * gb[c][i] + gb[c][8 + i];
       Vec8<T>::store(y + (long)row * ldy + ch * 8, o);
     }
   }
@@ -267,6 +270,8 @@ extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long l
                                   long ldy, float* mean, float* rstd, smer_stream_t stream) {
   SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_fwd: N % 8 == 0 and N <= 2048");
   SMER_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0, "smer_layernorm_fwd: strides % 8");
+  SMER_REQUIRE((((uintptr_t)gamma | (uintptr_t)beta) & 15) == 0,
+               "smer_layernorm_fwd: gamma / beta must be 16-B aligned");
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((M + 3) / 4);

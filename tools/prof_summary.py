@@ -13,3 +13,11 @@ for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:int(sys.argv[
                                           float(r['TotalDurationNs']) / 1e6 / steps,
                                           100 * float(r['TotalDurationNs']) / tot))
 print("total kernel time per step: %.3f ms" % (tot / 1e6 / steps))
+fam = [r for r in rows if r['Name'].replace('void ', '').startswith(
+    ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm_skinny_bf16_kernel"))]
+red = [r for r in rows if r['Name'].startswith("splitk_reduce_kernel")]
+if fam:
+    calls = sum(int(r['Calls']) for r in fam)
+    ns = sum(float(r['TotalDurationNs']) for r in fam + red)
+    print("smer_gemm family (tile kernels + split-K reduce): %d calls, %.2f us per smer_gemm call, "
+          "%.3f ms/step" % (calls, ns / 1e3 / calls, ns / 1e6 / steps))

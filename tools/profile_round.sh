@@ -1,6 +1,7 @@
 #!/bin/bash
 # Profile the headline bench: kernel-trace stats + separate PMC passes for
-# FETCH_SIZE and WRITE_SIZE (never combined with other tracing domains).
+# FETCH_SIZE and WRITE_SIZE (never combined with other tracing domains),
+# plus the decode step (graph replays).
 # Usage (on the GPU box, from the repo root): bash tools/profile_round.sh <tag>
 set -e
 export TMPDIR=/tmp
@@ -10,8 +11,10 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $R/bench.py --steps 5 --warmup 2 --no-infill --no-cpu > $OUT/trace.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
   python3 $R/bench.py --steps 2 --warmup 1 --no-infill --no-cpu --no-roofline > $OUT/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
   python3 $R/bench.py --steps 2 --warmup 1 --no-infill --no-cpu --no-roofline > $OUT/write.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dec -o run -- \
+  python3 $R/tools/prof_decode.py --n 50 --graph > $OUT/dec.log 2>&1
 echo done
