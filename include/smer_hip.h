@@ -43,6 +43,10 @@
  *                        linears, train.py:783)
  *   smer_colsum          bias gradients (autograd of nn.Linear bias)
  *   smer_cast            fp32 master -> bf16 working copies
+ *   smer_fp8_quantize    per-tensor e4m3 quantisation (amax + scaled cast) of
+ *                        a bf16 activation / weight for the fp8 GEMM
+ *   smer_gemm_fp8        fp8 (e4m3 x e4m3, fp32 accumulate) forward Linear of
+ *                        the QKV / FFN contractions (BASELINE C4)
  */
 #ifndef SMER_HIP_H
 #define SMER_HIP_H
@@ -219,6 +223,20 @@ size_t smer_colsum_workspace(int M, int N);
 /* out[n] (+)= sum_m x[m, n] (deterministic two-stage). */
 int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, int accumulate,
                 void* workspace, size_t ws_bytes, smer_stream_t stream);
+
+/* fp8 (OCP e4m3), per-tensor scaled.  smer_fp8_quantize: q[rows, cols] =
+ * e4m3(x * 448 / amax|x|), *inv_scale = amax / 448 (device float, no host
+ * sync); workspace = smer_fp8_quantize_workspace() bytes (16-B aligned).
+ * smer_gemm_fp8: C[M,N] bf16 = (a_inv * b_inv) * A8[M,K] . B8[N,K]^T + bias
+ * (+ReLU) (+dropout) (+residual); M, N % 256 == 0, K % 128 == 0, else
+ * SMER_ERR_UNSUPPORTED (callers fall back to bf16). */
+size_t smer_fp8_quantize_workspace(void);
+int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, void* q, long ldq,
+                      void* workspace, float* inv_scale, smer_stream_t stream);
+int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                  const float* a_inv, const float* b_inv, const float* bias, int relu,
+                  const void* residual, long ldr, float drop_p, uint32_t drop_seed, void* C,
+                  long ldc, smer_stream_t stream);
 
 #ifdef __cplusplus
 }

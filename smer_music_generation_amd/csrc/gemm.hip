@@ -1102,3 +1102,239 @@ extern "C" int smer_linear_decode(int M, int N, int K, const void* A, long lda, 
   SMER_CHECK_LAUNCH("smer_linear_decode");
   return SMER_OK;
 }
+
+// ---------------------------------------------------------------------------
+// fp8 (OCP e4m3) forward GEMM, per-tensor scaled (BASELINE C4: "fp8 MFMA
+// GEMMs on CDNA4").  C = (a_inv * b_inv) * A8 . B8^T + epilogue, where
+// A8 = e4m3(A * 448 / amax(A)) and a_inv = amax(A) / 448 (likewise B).
+// MFMA: the block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0
+// scales (127) — the K = 128 form runs at the fp8 rate, 2x bf16 (the plain
+// 16x16x32 fp8 MFMA runs at the bf16 rate).  Tile / staging as the bf16
+// 256x256 kernel: a K stage is 128 fp8 = 128 B per row, so the LDS image
+// (128-B rows, 16-B chunks XOR (row & 7)) and its LDS-DMA fill are the same
+// bytes; a 16x16x128 fragment is 32 B per lane (two chunks).
+// ---------------------------------------------------------------------------
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+namespace {
+constexpr int F8K = 128;  // K per stage (bytes per row)
+
+__device__ __forceinline__ void f8_glds(char* buf, const uint8_t* P, long ld, int rows, int r0,
+                                        int k0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int chunk = wave * 4 + c;  // 32 x 1 KiB = 256 rows x 128 B
+    const int row = chunk * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (row & 7);
+    const uint8_t* src = P + (long)min(r0 + row, rows - 1) * ld + k0 + lc * 16;
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
+  }
+}
+// lane (c16, g): row rbase + c16, k bytes [32g, 32g + 32) = chunks 2g, 2g + 1
+__device__ __forceinline__ i32x8 f8_frag(const char* buf, int rbase, int lane) {
+  const int g = lane >> 4, row = rbase + (lane & 15);
+  const uint4 lo = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g) ^ (row & 7)) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g + 1) ^ (row & 7)) << 4));
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+__device__ __forceinline__ f32x4 mfma_f8(i32x8 a, i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K,
+                                                             const uint8_t* __restrict__ A, long lda,
+                                                             const uint8_t* __restrict__ B, long ldb,
+                                                             const float* __restrict__ a_inv,
+                                                             const float* __restrict__ b_inv,
+                                                             GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nbm = M / G2, nbn = N / G2;
+  const int nwg = nbm * nbn;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  const int nk = K / F8K;
+  GemmEpi ee = e;
+  ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int wgid = xstart + jj;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int m0 = (first_m + within % gsz) * G2, n0 = (within / gsz) * G2;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    f8_glds(smem, A, lda, M, m0, 0, tid);
+    f8_glds(smem + G2_OP, B, ldb, N, n0, 0, tid);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // stage kt landed; stage kt-1 fully read
+      if (kt + 1 < nk) {
+        char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
+        f8_glds(nb, A, lda, M, m0, (kt + 1) * F8K, tid);
+        f8_glds(nb + G2_OP, B, ldb, N, n0, (kt + 1) * F8K, tid);
+      }
+      const char* a_s = smem + (kt & 1) * G2_STAGE;
+      const char* b_s = a_s + G2_OP;
+      i32x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(b_s, wn * 64 + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const i32x8 af = f8_frag(a_s, wm * 128 + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f8(af, bfr[j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+
+    const int g = lane >> 4, c16 = lane & 15;
+    constexpr int EP_LD = G2 + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      if (wm == (pass >> 1)) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = 4 * (pass & 1) + ii;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
+        const int row = item >> 5, ch = item & 31;
+        const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+        const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_apply8(ee, M, N, grow, gcol, v);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// amax(|x|) over a [rows, cols] bf16 view: float bits of non-negative values
+// order like unsigned ints, so an integer atomicMax is exact and the result
+// does not depend on the order of arrival.
+__global__ __launch_bounds__(256) void amax_bf16_kernel(int rows, int cols, const bf16* __restrict__ x,
+                                                       long ldx, unsigned int* __restrict__ out) {
+  const int cpr = cols >> 3;
+  const long n = (long)rows * cpr;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cpr, c = (i % cpr) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + r * ldx + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)v[k]));
+  }
+  m = wave_max(m);
+  __shared__ float wm_[4];
+  if ((threadIdx.x & 63) == 0) wm_[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm_[0], wm_[1]), fmaxf(wm_[2], wm_[3]));
+    atomicMax(out, __float_as_uint(m));
+  }
+}
+
+// q = e4m3(x * 448 / amax) (round to nearest even, saturating), inv = amax / 448
+__global__ __launch_bounds__(256) void quant_fp8_kernel(int rows, int cols, const bf16* __restrict__ x,
+                                                       long ldx, uint8_t* __restrict__ q, long ldq,
+                                                       const unsigned int* __restrict__ amax,
+                                                       float* __restrict__ inv) {
+  const float am = __uint_as_float(*amax);
+  const float sc = am > 0.f ? 448.f / am : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *inv = 1.f / sc;
+  const int cpr = cols >> 3;
+  const long n = (long)rows * cpr;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cpr, c = (i % cpr) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + r * ldx + c);
+    uint32_t w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float f[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f[k] = fminf(fmaxf((float)v[4 * h + k] * sc, -448.f), 448.f);
+      int p = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+      p = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], p, true);
+      w[h] = (uint32_t)p;
+    }
+    *reinterpret_cast<uint2*>(q + r * ldq + c) = make_uint2(w[0], w[1]);
+  }
+}
+
+extern "C" size_t smer_fp8_quantize_workspace(void) { return 16; }
+
+extern "C" int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, void* q, long ldq,
+                                 void* workspace, float* inv_scale, smer_stream_t stream) {
+  SMER_REQUIRE(rows >= 0 && cols > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldq % 8 == 0,
+               "smer_fp8_quantize: cols / strides must be multiples of 8");
+  SMER_REQUIRE(x && q && workspace && inv_scale && aligned16(x) && ((uintptr_t)q & 7) == 0,
+               "smer_fp8_quantize: pointers / alignment");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned int* am = (unsigned int*)workspace;
+  if (hipMemsetAsync(am, 0, sizeof(unsigned int), s) != hipSuccess)
+    return smer_set_error(SMER_ERR_HIP, "smer_fp8_quantize: memset");
+  const long n = (long)rows * (cols / 8);
+  const int grid = (int)std::max<long>(1, std::min<long>((n + 255) / 256, 8L * smer_num_cus()));
+  hipLaunchKernelGGL(amax_bf16_kernel, dim3(grid), dim3(256), 0, s, rows, cols, (const bf16*)x, ldx, am);
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3(grid), dim3(256), 0, s, rows, cols, (const bf16*)x, ldx,
+                     (uint8_t*)q, ldq, (const unsigned int*)am, inv_scale);
+  SMER_CHECK_LAUNCH("smer_fp8_quantize");
+  return SMER_OK;
+}
+
+extern "C" int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                             const float* a_inv, const float* b_inv, const float* bias, int relu,
+                             const void* residual, long ldr, float drop_p, uint32_t drop_seed,
+                             void* C, long ldc, smer_stream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % G2 || N % G2 || K % F8K)
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm_fp8: needs M, N % 256 == 0 and K % 128 == 0");
+  SMER_REQUIRE(A && B && C && a_inv && b_inv, "smer_gemm_fp8: null pointer");
+  SMER_REQUIRE(lda % 16 == 0 && ldb % 16 == 0 && aligned16(A) && aligned16(B),
+               "smer_gemm_fp8: operand strides / alignment");
+  SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_gemm_fp8: drop_p out of range");
+  GemmEpi e{};
+  e.bias = bias; e.alpha = 1.f; e.relu = relu; e.residual = residual; e.ldr = ldr;
+  e.drop_thr = smer_drop_thr16(drop_p); e.seed = drop_seed;
+  e.drop_scale = smer_drop_scale16(e.drop_thr);
+  e.C = C; e.ldc = ldc;
+  auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
+  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc);
+  hipStream_t s = (hipStream_t)stream;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm256_fp8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        2 * G2_STAGE);
+    attr_set = true;
+  }
+  const long tiles = (long)(M / G2) * (N / G2);
+  const int grid = tiles > smer_num_cus() ? (smer_num_cus() & ~7) : (int)tiles;
+  hipLaunchKernelGGL(gemm256_fp8_kernel, dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
+                     (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  SMER_CHECK_LAUNCH("smer_gemm_fp8");
+  return SMER_OK;
+}

@@ -248,6 +248,32 @@ def linear_decode(x, w, bias=None, *, relu=False, residual=None, out=None, out_f
     return out if out is not None else out_f32
 
 
+# ---------------------------------------------------------------------------
+def fp8_quantize(x, q, inv_scale, workspace=None):
+    """q (uint8 e4m3 bits, same shape as x) = e4m3(x * 448 / amax|x|);
+    inv_scale (1-element fp32, device) = amax / 448."""
+    rows, cols = x.shape
+    if workspace is None:
+        workspace = torch.empty(16, dtype=torch.uint8, device=x.device)
+    call("smer_fp8_quantize", rows, cols, _p(x), _ld(x), _p(q), _ld(q), _p(workspace),
+         _p(inv_scale), _stream())
+    return q
+
+
+def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
+             seed=0):
+    """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ epilogue).  Returns False
+    (nothing launched) when the shape is outside the fp8 kernel's tiling."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    if M % 256 or N % 256 or K % 128:
+        return False
+    call("smer_gemm_fp8", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
+         _p(bias), int(bool(relu)), _p(residual), _ld(residual) if residual is not None else 0,
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out), _stream())
+    return True
+
+
 def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, out_tok, alive, *,
                         eos, m0, trash_pos, max_span=100):
     R, nst = state.shape

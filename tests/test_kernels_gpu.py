@@ -574,3 +574,54 @@ def test_linear_decode_kv_scatter(M, N, K):
     torch.cuda.synchronize()
     assert rel_err(out, ref) < 2e-2
     assert torch.equal(cache[req.long(), pos.long()], out[:, col0:])
+
+
+# ------------------------------------------------------------ fp8
+def test_gemm_fp8_exact_integer_layout():
+    """fp8 MFMA fragment / output layout with exact small-integer e4m3 data
+    and an asymmetric B: the kernel must reproduce A.B^T exactly."""
+    O = ops()
+    M, N, K = 256, 512, 384
+    g = torch.Generator(device="cpu").manual_seed(0)
+    A = torch.randint(-4, 5, (M, K), generator=g).float()
+    B = torch.randint(-3, 4, (N, K), generator=g).float()
+    B[:, 0] += torch.arange(N) % 5  # asymmetric
+    a8 = A.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    b8 = B.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    one = torch.ones(1, device=dev)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    assert O.gemm_fp8(a8, one, b8, one, C)
+    ref = A.to(torch.float8_e4m3fn).float() @ B.to(torch.float8_e4m3fn).float().t()
+    torch.cuda.synchronize()
+    assert torch.equal(C.float().cpu(), ref.to(torch.bfloat16).float())
+
+
+def test_fp8_quantize_and_gemm():
+    """Per-tensor quantisation (amax + scaled e4m3 cast, matching torch's
+    float8_e4m3fn rounding) and the scaled fp8 GEMM with the full epilogue
+    against fp32."""
+    O = ops()
+    M, N, K = 512, 768, 768
+    x = (torch.randn(M, K, device=dev) * 3).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) * 0.05).to(torch.bfloat16)
+    x8 = torch.empty(M, K, device=dev, dtype=torch.uint8)
+    w8 = torch.empty(N, K, device=dev, dtype=torch.uint8)
+    xi = torch.empty(1, device=dev)
+    wi = torch.empty(1, device=dev)
+    O.fp8_quantize(x, x8, xi)
+    O.fp8_quantize(w, w8, wi)
+    torch.cuda.synchronize()
+    amax = x.float().abs().max()
+    assert abs(xi.item() - amax.item() / 448) < 1e-6 * amax.item()
+    ref8 = (x.float() * (448 / amax)).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    agree = (ref8 == x8).float().mean().item()
+    assert agree > 0.999, agree
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    assert O.gemm_fp8(x8, xi, w8, wi, C, bias=bias, relu=True, residual=res)
+    ref = torch.relu(x.float() @ w.float().t() + bias) + res.float()
+    torch.cuda.synchronize()
+    err = ((C.float() - ref).norm() / ref.norm()).item()
+    assert err < 0.05, err
+    assert not O.gemm_fp8(x8[:100], xi, w8, wi, C[:100])  # outside the tiling: caller falls back
