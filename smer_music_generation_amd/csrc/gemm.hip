@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         for (int i = 0; i < 4; ++i) af[i] = frag<AK>(a_s, wm * 64 + i * 16, s, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+        __builtin_amdgcn_sched_barrier(0);  // all 8 fragment reads, then the 16 MFMAs
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -541,15 +542,18 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
       const char* b_s = a_s + G2_OP;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 bfr[4];
+        // the k-step's 12 fragment reads first, then its 32 MFMAs (else the
+        // compiler waits on each A fragment right behind 4 MFMAs)
+        bf16x8 bfr[4], af[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bf16x8 af = g2_frag<AK>(a_s, wm * 128 + i * 16, s, lane);
+        for (int i = 0; i < 8; ++i) af[i] = g2_frag<AK>(a_s, wm * 128 + i * 16, s, lane);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af, bfr[j], acc[i][j]);
-        }
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
