@@ -53,6 +53,8 @@ class Engine:
         self._bf16 = None
         self._bf16_version = None
         self._fc_pad = None
+        self._wgen = 0          # bumped whenever the working weights are rewritten
+        self._ckv_all = None    # (key, W [L*2d, d], b [L*2d]) stacked cross-attn K/V projections
 
     # ------------------------------------------------------------------
     def act_dtype(self):
@@ -69,6 +71,7 @@ class Engine:
             ops.cast(flat, self._bf16)
             self._fc_pad = None
             self._bf16_version = ver
+            self._wgen += 1
         return self._bf16
 
     def _version_key(self):
@@ -81,6 +84,7 @@ class Engine:
         """Called by the fused Adam, which rewrites the bf16 copy itself."""
         self._bf16_version = self._version_key()
         self._fc_pad = None
+        self._wgen += 1
 
     def weights(self, dt):
         """Per-layer views of the working weights (bf16 copy or fp32 master);
@@ -135,6 +139,21 @@ class Engine:
             self._fc_pad = torch.zeros(self.Vp, d, dtype=dt, device=work.device)
         ops.cast(W.fc_w.reshape(-1), self._fc_pad[:V].reshape(-1))
         W.fc_pad = self._fc_pad
+        # The decoder's cross-attention K/V projections all read the encoder
+        # memory: stacked [L*2d, d] they run as ONE GEMM in the forward
+        # (memory -> every layer's K|V) and ONE dgrad GEMM (K = L*2d) in the
+        # backward instead of L each.  Rebuilt when the weights change.
+        key = (dt, work.data_ptr(), self._wgen, self._version_key())
+        if self.n_dec and (self._ckv_all is None or self._ckv_all[0] != key):
+            n2 = 2 * d
+            wall = torch.empty(self.n_dec * n2, d, dtype=dt, device=work.device)
+            ball = torch.empty(self.n_dec * n2, device=work.device)
+            for i, L in enumerate(W.dec):
+                ops.cast2d(L.ckv_w, wall[i * n2:(i + 1) * n2])
+                ops.cast(L.ckv_b, ball[i * n2:(i + 1) * n2])
+            self._ckv_all = (key, wall, ball)
+        if self.n_dec:
+            W.ckv_all, W.ckv_b_all = self._ckv_all[1], self._ckv_all[2]
         return W
 
     def grad_views(self):
@@ -251,6 +270,8 @@ class Engine:
         y = torch.empty(B * T, d, dtype=dt, device=dev)
         ops.embed(tgt_ids, W.emb, pe2, y, L=T, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_tgt"]))
         wts = torch.empty(self.n_dec, B, T, S, device=dev) if need_weights else None
+        # every decoder layer's cross-attention K|V of the memory, one GEMM
+        kvc_all = ops.linear(mem, W.ckv_all, W.ckv_b_all) if self.n_dec else None
         for i, L in enumerate(W.dec):
             qkv = ops.linear(y, L.sa_w, L.sa_b)
             o = torch.empty(B * T, d, dtype=dt, device=dev)
@@ -261,7 +282,7 @@ class Engine:
             y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr, seed=sd(_site("dec", i, 1)))
             x1, m1, r1 = self._ln(y1, L.n1, dt)
             qc = ops.linear(x1, L.cq_w, L.cq_b)
-            kvc = ops.linear(mem, L.ckv_w, L.ckv_b)
+            kvc = kvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             oc = torch.empty(B * T, d, dtype=dt, device=dev)
             lsec = torch.empty(B, H, T, device=dev)
             ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
@@ -313,7 +334,9 @@ class Engine:
                           dbeta=G.dec_norm[1])
         if hook:
             hook("head")
-        dmem = torch.zeros(Ms, d, device=dev)
+        # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
+        # one dgrad GEMM (K = L*2d) after the decoder loop gives dmemory
+        dkvc_all = torch.empty(Ms, self.n_dec * 2 * d, dtype=dt, device=dev)
         for i in reversed(range(self.n_dec)):
             L, GL = W.dec[i], G.dec[i]
             (y_in, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2, h, y3, m3,
@@ -335,13 +358,12 @@ class Engine:
             doc = ops.linear_dgrad(dy2d, L.ca_ow)
             ops.linear_wgrad(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
-            dkvc = torch.empty(Ms, 2 * d, dtype=dt, device=dev)
+            dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)))
             dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
             ops.linear_wgrad(dqc, x1, GL.cq_w, db=GL.cq_b)
-            ops.linear_dgrad(dkvc, L.ckv_w, out_f32=dmem, accumulate=True)
             ops.linear_wgrad(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
             # self-attention block
             dy1 = torch.empty_like(y1)
@@ -360,6 +382,10 @@ class Engine:
             if hook:
                 hook("dec%d" % i)
         d_tgt = dy
+        if self.n_dec:
+            dmem = ops.linear_dgrad(dkvc_all, W.ckv_all, out_f32=torch.empty(Ms, d, device=dev))
+        else:
+            dmem = torch.zeros(Ms, d, device=dev)
         # encoder
         x_last, me, re = ctx.enc_last
         dx = torch.empty_like(x_last)
