@@ -85,7 +85,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
 
 constexpr int LN_BWD_ROWS = 64;  // rows per workgroup (16 per wave)
 
-template <typename T, bool DYF>
+// One wave per row, NC 16-B chunks per lane (N <= 512 * NC); a wave takes
+// its 16 rows of the block RB at a time with all RB rows' loads issued
+// together (the rows are otherwise a chain of dependent HBM round trips at
+// 2 waves per SIMD).  Column partials for dgamma / dbeta accumulate in a
+// fixed row order (deterministic).
+template <typename T, bool DYF, int NC, int RB>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* __restrict__ dyv,
                                                      long lddy, const T* __restrict__ x, long ldx,
                                                      const float* __restrict__ mean,
@@ -95,56 +100,82 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
                                                      T* __restrict__ dxd, long ldxd,
                                                      uint32_t thr, uint32_t seed, float dscale,
                                                      float* __restrict__ part) {
+  constexpr int LN_MAXC = NC;
   __shared__ float red[4][2][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nch = N >> 3;
-  float pg[LN_MAXC][8], pb[LN_MAXC][8];
+  float pg[NC][8], pb[NC][8], gm[NC][8];
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c)
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) Vec8<float>::load(gamma + ch * 8, gm[c]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { pg[c][i] = 0.f; pb[c][i] = 0.f; }
+  }
   const int r0 = blockIdx.x * LN_BWD_ROWS;
-  for (int rr = wave; rr < LN_BWD_ROWS; rr += 4) {
-    const int row = r0 + rr;
-    if (row >= M) break;
-    const float mu = mean[row], rs = rstd[row];
-    const uint32_t rowkey = thr ? smer_rowkey(seed, (uint32_t)row) : 0u;
-    float xh[LN_MAXC][8], gd[LN_MAXC][8];
-    float s1 = 0.f, s2 = 0.f;
+  for (int rb = 0; rb < LN_BWD_ROWS / 4; rb += RB) {
+    float xh[RB][NC][8], gd[RB][NC][8], mu[RB], rs[RB];
+    bool ok[RB];
 #pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-      int ch = lane + 64 * c;
-      if (ch < nch) {
-        float xv[8], dv[8];
-        Vec8<T>::load(x + (long)row * ldx + ch * 8, xv);
-        if (DYF) Vec8<float>::load((const float*)dyv + (long)row * lddy + ch * 8, dv);
-        else Vec8<T>::load((const T*)dyv + (long)row * lddy + ch * 8, dv);
+    for (int u = 0; u < RB; ++u) {
+      const int row = r0 + wave + 4 * (rb + u);
+      ok[u] = row < M;
+      mu[u] = ok[u] ? mean[row] : 0.f;
+      rs[u] = ok[u] ? rstd[row] : 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float h = (xv[i] - mu) * rs;
-          float gg = dv[i] * gamma[ch * 8 + i];
-          xh[c][i] = h;
-          gd[c][i] = gg;
-          s1 += gg;
-          s2 += gg * h;
-          pg[c][i] += dv[i] * h;
-          pb[c][i] += dv[i];
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ok[u] && ch < nch) {
+          Vec8<T>::load(x + (long)row * ldx + ch * 8, xh[u][c]);
+          if (DYF) Vec8<float>::load((const float*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
+          else Vec8<T>::load((const T*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
         }
       }
     }
-    s1 = wave_sum(s1) / N;
-    s2 = wave_sum(s2) / N;
+    float s1[RB], s2[RB];
 #pragma unroll
-    for (int c = 0; c < LN_MAXC; ++c) {
-      int ch = lane + 64 * c;
-      if (ch < nch) {
-        float o[8];
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = 0.f;
+      s2[u] = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = rs * (gd[c][i] - s1 - xh[c][i] * s2);
-        Vec8<T>::store(dx + (long)row * lddx + ch * 8, o);
-        if (dxd) {
-          if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)(ch * 8), o);
-          Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ok[u] && ch < nch)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float dv = gd[u][c][i];
+            const float h = (xh[u][c][i] - mu[u]) * rs[u];
+            const float gg = dv * gm[c][i];
+            xh[u][c][i] = h;
+            gd[u][c][i] = gg;
+            s1[u] += gg;
+            s2[u] += gg * h;
+            pg[c][i] += dv * h;
+            pb[c][i] += dv;
+          }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = wave_sum(s1[u]) / N;
+      s2[u] = wave_sum(s2[u]) / N;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = r0 + wave + 4 * (rb + u);
+      const uint32_t rowkey = thr ? smer_rowkey(seed, (uint32_t)row) : 0u;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ok[u] && ch < nch) {
+          float o[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = rs[u] * (gd[u][c][i] - s1[u] - xh[u][c][i] * s2[u]);
+          Vec8<T>::store(dx + (long)row * lddx + ch * 8, o);
+          if (dxd) {
+            if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)(ch * 8), o);
+            Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
+          }
         }
       }
     }
@@ -309,14 +340,22 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   uint32_t thr = smer_drop_thr16(drop_p);
   float ds = smer_drop_scale16(thr);
   float* part = params ? (float*)workspace : nullptr;
-#define LNB(T, F)                                                                              \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, F>), dim3(nblk), dim3(256), 0, s, M, N, dy, lddy,       \
-                     (const T*)x, ldx, mean, rstd, gamma, (T*)dx, lddx, (T*)dx_drop, ldxd, thr, \
-                     seed, ds, part)
+  SMER_REQUIRE(((uintptr_t)gamma & 15) == 0, "smer_layernorm_bwd: gamma must be 16-B aligned");
+#define LNB1(T, F, NC, RB)                                                                     \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, F, NC, RB>), dim3(nblk), dim3(256), 0, s, M, N, dy,     \
+                     lddy, (const T*)x, ldx, mean, rstd, gamma, (T*)dx, lddx, (T*)dx_drop, ldxd, \
+                     thr, seed, ds, part)
+#define LNB(T, F)                                  \
+  do {                                             \
+    if (N <= 512) LNB1(T, F, 1, 4);                \
+    else if (N <= 1024) LNB1(T, F, 2, 2);          \
+    else LNB1(T, F, 4, 1);                         \
+  } while (0)
   if (dtype == SMER_BF16) { if (dy_f32) LNB(bf16, true); else LNB(bf16, false); }
   else if (dtype == SMER_F32) { LNB(float, false); }
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
+#undef LNB1
   if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
     smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s, dbeta, N);
