@@ -405,6 +405,122 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
+// 64x128 bf16 tile for the mid-size forward / dgrad shapes (decoder: M =
+// B*T = 8192, N = 512) where 128x128 tiles number ~one per CU and each CU
+// then runs a single 4-wave workgroup, exposing every stage's load
+// latency.  Halving the tile doubles the workgroups (3 resident per CU: 48
+// KiB of LDS, few registers).  4 waves as 2 x 2 of 32 x 64, LDS-DMA staging
+// of the same images as the 128 kernel (A: 64 K-contiguous rows; B: row or
+// column image of 128), one barrier per 64-deep K step, epilogue through
+// LDS in one 64-row pass.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int G64_A = 64 * GBK * 2;            // 8 KiB
+constexpr int G64_STAGE = G64_A + TILE_BYTES;  // + 16 KiB of B
+__device__ __forceinline__ void a64_glds(char* buf, const bf16* P, long ld, int rows, int r0,
+                                         int k0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int chunk = wave * 2 + c;  // 8 x 1 KiB: rows 8*chunk .. +7
+    const int row = chunk * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (row & 7);
+    const bf16* src = P + (long)min(r0 + row, rows - 1) * ld + k0 + lc * 8;
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
+  }
+}
+}  // namespace
+
+template <bool BKC>
+__global__ __launch_bounds__(256, 3) void gemm64_bf16_kernel(int M, int N, int K,
+                                                             const bf16* __restrict__ A, long lda,
+                                                             const bf16* __restrict__ B, long ldb,
+                                                             GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbm = (M + 63) / 64, nbn = (N + GBN - 1) / GBN;
+  const int nwg = nbm * nbn;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 8;
+  const int nk = K / GBK;
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int wgid = xstart + jj;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int m0 = (first_m + within % gsz) * 64, n0 = (within / gsz) * GBN;
+
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    a64_glds(smem, A, lda, M, m0, 0, tid);
+    stage_glds<BKC>(smem + G64_A, B, ldb, N, n0, 0, tid);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // stage kt landed; stage kt-1 fully read
+      if (kt + 1 < nk) {
+        char* nb = smem + ((kt + 1) & 1) * G64_STAGE;
+        a64_glds(nb, A, lda, M, m0, (kt + 1) * GBK, tid);
+        stage_glds<BKC>(nb + G64_A, B, ldb, N, n0, (kt + 1) * GBK, tid);
+      }
+      const char* a_s = smem + (kt & 1) * G64_STAGE;
+      const char* b_s = a_s + G64_A;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af[2], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = frag<true>(a_s, wm * 32 + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+
+    const int g = lane >> 4, c16 = lane & 15;
+    constexpr int EP_LD = GBN + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ep[(wm * 32 + i * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int item = tid + 256 * c;  // 64 rows x 16 chunks of 8 columns
+      const int row = item >> 4, ch = item & 15;
+      const int grow = m0 + row, gcol = n0 + ch * 8;
+      if (grow < M && gcol < N) {
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+        const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        epi_apply8(e, M, N, grow, gcol, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 256x256 bf16 GEMM for the large-M forward (NT) and dgrad (NN) shapes.
 // 8 waves (2 along M x 4 along N), 128x64 outputs per wave: per 32-deep
 // k-step a wave reads 8 A + 4 B fragments for 32 MFMAs, and per K tile the
@@ -902,6 +1018,16 @@ static bool smer_gemm256_enabled() {
   return v == 1;
 }
 
+// SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests)
+static bool smer_gemm64_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_GEMM64");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static int smer_num_cus() {
   static int cache[64] = {0};
   int dev = 0;
@@ -981,6 +1107,16 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   }
   int tiles = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   int split = choose_split(M, N, K, e, ws ? ws_bytes : 0);
+  // mid-size forward / dgrad: fewer 128x128 tiles than two per CU -> 64x128
+  if (AK && !rowsum && split == 1 && K % GBK == 0 && tiles <= 4 * smer_num_cus() &&
+      M > 4 * SK_BM && smer_gemm_glds_enabled() && smer_gemm64_enabled()) {
+    const long t64 = (long)((M + 63) / 64) * ((N + GBN - 1) / GBN);
+    const long res = 3L * smer_num_cus();
+    const int grid = t64 > res ? (int)(res & ~7L) : (int)t64;
+    hipLaunchKernelGGL((gemm64_bf16_kernel<BKC>), dim3(grid), dim3(256), 2 * G64_STAGE, s, M, N, K,
+                       (const bf16*)A, lda, (const bf16*)B, ldb, e);
+    return;
+  }
   int kchunk = K;
   if (split > 1) {
     kchunk = ((K + split - 1) / split + GBK - 1) / GBK * GBK;

@@ -625,3 +625,30 @@ def test_fp8_quantize_and_gemm():
     err = ((C.float() - ref).norm() / ref.norm()).item()
     assert err < 0.05, err
     assert not O.gemm_fp8(x8[:100], xi, w8, wi, C[:100])  # outside the tiling: caller falls back
+
+
+@pytest.mark.parametrize("M,N,K,bk", [(1000, 264, 512, True), (8192, 512, 512, False),
+                                      (777, 512, 1536, True)])
+def test_gemm64_mid_size_epilogues(M, N, K, bk):
+    """The 64x128 tile kernel (mid-size M: fewer 128x128 tiles than two per
+    CU) with ragged M / N tails: bias + ReLU + dropout + residual, and a
+    ReLU-grad gate."""
+    O = ops()
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    Wm = W if bk else W.t().contiguous()
+    bias = torch.randn(N, device=dev)
+    R = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    p, seed = 0.1, 11
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, bias=bias, relu=True, residual=R, drop_p=p,
+           seed=seed)
+    base = A.float() @ W.float().t()
+    keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 2e-2
+    O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, gate=R, gate_scale=1.5)
+    ref = torch.where(R.float() > 0, base * 1.5, torch.zeros_like(base))
+    torch.cuda.synchronize()
+    assert rel_err(C, ref) < 2e-2
