@@ -102,6 +102,18 @@ def bench_train(args, dev, rank, world):
     return res
 
 
+def bench_train_c4(args, dev, rank, world):
+    """BASELINE.json configs[3] / SURVEY §8 C4 shapes: 12 + 12 layers, d_model
+    768, 12 heads, FF 2048, per-GPU B=32 sources of S=2048 and T=512 decoder
+    tokens, dropout 0.1, the full train step in bf16 (the fp8 GEMM kernel is
+    a separate building block, tools/bench_fp8.py)."""
+    import copy
+    a = copy.copy(args)
+    a.layers, a.d_model, a.nhead, a.seq, a.tgt = 12, 768, 12, 2048, 512
+    a.steps, a.warmup, a.roofline = args.c4_steps, args.c4_warmup, False
+    return bench_train(a, dev, rank, world)
+
+
 def _infill_requests(n, target_len=1024, seed0=0, n_infill_bars=2):
     """n synthetic 3-track songs of ~target_len SMER tokens, each request
     infilling one track over its last-but-two n_infill_bars bars."""
@@ -239,6 +251,9 @@ def parse_args(argv=None):
     ap.add_argument("--infill-batch", dest="infill_batch", type=int, default=32)
     ap.add_argument("--no-infill", dest="infill", action="store_false")
     ap.add_argument("--no-c5", dest="c5", action="store_false")
+    ap.add_argument("--no-c4", dest="c4", action="store_false")
+    ap.add_argument("--c4-steps", dest="c4_steps", type=int, default=3)
+    ap.add_argument("--c4-warmup", dest="c4_warmup", type=int, default=1)
     ap.add_argument("--c5-requests", dest="c5_requests", type=int, default=64)
     ap.add_argument("--c5-seq", dest="c5_seq", type=int, default=4096)
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
@@ -260,6 +275,7 @@ def main():
     _lib.load()
 
     tr = bench_train(args, dev, rank, world)
+    c4 = bench_train_c4(args, dev, rank, world) if args.c4 else None
     inf = None
     if args.infill:
         inf = bench_infill(args, dev, rank)
@@ -315,6 +331,14 @@ def main():
                                "mean_src_len": round(inf["mean_src_len"], 1),
                                "decode_steps": inf["steps"], "tokens": inf["tokens"],
                                "phases_s": inf["phases_s"], "parallelism": "replicas"},
+            "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
+                                          "S=2048 T=512, bf16",
+                                "value": round(c4["tokens_per_s"], 1),
+                                "ms_per_step": round(c4["ms_per_step"], 2),
+                                "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),
+                                "mfma_frac_whole_step": round(c4["mfma_frac_whole_step"], 4),
+                                "global_batch": args.batch * world, "steps": args.c4_steps,
+                                "parallelism": "dp%d" % world},
             "infill_c5": c5 and {"metric": "C5 batched infill tokens/s (64 requests x ~4096-token "
                                            "sources, 4 bars of one track each, greedy)",
                                  "value": round(c5["tokens_per_s"], 1),
