@@ -106,10 +106,17 @@ int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long ld
  * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:
  * key j visible to query i iff j <= i.  lse: fp32 [B, H, Lq] (natural log).
  * Attention-probability dropout with (drop_p, seed). */
+/* Attention-dropout keep bits of a [B*H, Lq, Lk] score matrix, exactly the
+ * words smer_attn_fwd publishes when it hashes them itself (layout: see
+ * smer_attn_drop_mask_bytes); smer_attn_fwd(..., drop_mask, drop_mask_in = 1)
+ * then reads them instead of hashing (the forward is VALU-bound). */
+int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_p, uint32_t seed, void* mask,
+                            smer_stream_t stream);
 int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D,
                   const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                   void* o, long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
-                  float drop_p, uint32_t seed, void* drop_mask, smer_stream_t stream);
+                  float drop_p, uint32_t seed, void* drop_mask, int drop_mask_in,
+                  smer_stream_t stream);
 /* drop_mask (nullable, 16-B aligned, smer_attn_drop_mask_bytes): with
  * drop_p > 0 the bf16 forward also stores its keep bits (1 bit per
  * (query, key), as four 64-bit wave ballots per 16x16 block) so that

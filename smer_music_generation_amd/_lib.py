@@ -28,7 +28,8 @@ SIGNATURES = {
     "smer_gemm_wgrad_bias": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
                                      c_int, P, c_int, P, c_size, P]),
     "smer_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P,
-                              c_long, P, c_long, P, P, c_int, c_float, c_float, c_u32, P, P]),
+                              c_long, P, c_long, P, P, c_int, c_float, c_float, c_u32, P, c_int, P]),
+    "smer_attn_drop_mask_gen": (c_int, [c_int, c_int, c_int, c_int, c_float, c_u32, P, P]),
     "smer_attn_drop_mask_bytes": (c_size, [c_int, c_int, c_int, c_int]),
     "smer_attn_bwd_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "smer_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P,

@@ -93,7 +93,10 @@ __device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
 // QG query groups of 16 per wave (block = 64*QG queries): K / V fragments
 // read from LDS once per wave feed QG groups, halving LDS traffic per MFMA
 // at QG = 2 (the forward is otherwise LDS-bandwidth co-limited).
-template <int D, int QG, bool DROP>
+// MIN: the keep words come precomputed (attn_drop_mask_gen_kernel) instead
+// of being hashed here: the forward is VALU-bound and the hash (two 32-bit
+// multiplies per key pair) is as much VALU work as the softmax itself.
+template <int D, int QG, bool DROP, bool MIN = false>
 __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
                                                      const bf16* __restrict__ q, long ldq,
                                                      const bf16* __restrict__ k, long ldk,
@@ -175,6 +178,14 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
+    uint32_t mw[QG];
+    if constexpr (DROP && MIN) {
+#pragma unroll
+      for (int gq = 0; gq < QG; ++gq) {
+        const int q16 = min((q0w + gq * 16) >> 4, nq16 - 1);
+        mw[gq] = reinterpret_cast<const uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane];
+      }
+    }
     f32x4 st[QG][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
@@ -225,7 +236,16 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
           p[mt][r] = fast_exp2(fmaf(st[gq][mt][r], c, -mc));
           l_run[gq] += p[mt][r];
         }
-      if (DROP) {
+      if (DROP && MIN) {
+        // this lane's keep word of (query 16-block, key tile): bit 4mt + r
+        const int q16 = (q0w + gq * 16) >> 4;
+        const uint32_t mword = min(q16, nq16 - 1) == q16 ? mw[gq] : 0u;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            p[mt][r] = ((mword >> (mt * 4 + r)) & 1u) ? p[mt][r] * drop_scale : 0.f;
+      } else if (DROP) {
         // keys mt*16+4g+{0,1} and {2,3} share one hash; the keep bits are
         // also published as the 16x16 sub-block's four ballots (see
         // smer_drop_mask_bytes) so the backward reads instead of re-hashing
@@ -1123,6 +1143,36 @@ __global__ void kv_scatter_heads_kernel(int n_rows, int H, int D, const T* __res
       *reinterpret_cast<const uint4*>(src + (long)m * lds + col);
 }
 
+// The attention-dropout keep words of a whole [B*H, Lq, Lk] score matrix,
+// bit for bit what attn_fwd_bf16 (hashing path) publishes: word [bh][q16][t]
+// [lane (g, c)] holds query 16*q16 + c, key 64t + 16mt + 4g + r at bit
+// 4mt + r (smer_attn_drop_mask_bytes).  Pure integer VALU at full occupancy.
+__global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(long nwords, int Lq, int nq16, int nkt,
+                                                                uint32_t thr, uint32_t seed,
+                                                                uint16_t* __restrict__ out) {
+  const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwords) return;
+  const int lane = (int)(w & 63);
+  const long rest = w >> 6;
+  const int t = (int)(rest % nkt);
+  const long r2 = rest / nkt;
+  const int q16 = (int)(r2 % nq16);
+  const long bh = r2 / nq16;
+  const int g = lane >> 4, c = lane & 15;
+  const uint32_t rowkey = smer_rowkey(seed, (uint32_t)(bh * Lq + q16 * 16 + c));
+  const uint32_t pb = (uint32_t)(t * (KVB / 2) + 2 * g);
+  uint32_t mword = 0u;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+      const uint32_t hb = smer_pair_bits(rowkey, pb + mt * 8 + rp);
+      mword |= (uint32_t)((hb & 0xFFFFu) >= thr) << (mt * 4 + 2 * rp);
+      mword |= (uint32_t)((hb >> 16) >= thr) << (mt * 4 + 2 * rp + 1);
+    }
+  out[w] = (uint16_t)mword;
+}
+
 // ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
@@ -1132,12 +1182,15 @@ template <int D>
 static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
                             long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
                             const uint8_t* kpm, int causal, float scale, uint32_t thr,
-                            uint32_t seed, float ds, uint64_t* mask, hipStream_t s) {
+                            uint32_t seed, float ds, uint64_t* mask, int mask_in, hipStream_t s) {
   // two query groups per wave once there are enough blocks to fill the chip
   const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
   dim3 grid(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H);
-  auto kern = qg2 ? (thr ? attn_fwd_bf16<D, 2, true> : attn_fwd_bf16<D, 2, false>)
-                  : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>);
+  const bool min_ = thr && mask && mask_in;
+  auto kern = qg2 ? (min_ ? attn_fwd_bf16<D, 2, true, true>
+                          : (thr ? attn_fwd_bf16<D, 2, true> : attn_fwd_bf16<D, 2, false>))
+                  : (min_ ? attn_fwd_bf16<D, 1, true, true>
+                          : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>));
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
                      scale, thr, seed, ds, thr ? mask : nullptr);
@@ -1150,12 +1203,26 @@ extern "C" size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk) {
   return (size_t)B * H * ((Lq + 15) / 16) * ((Lk + 63) / 64) * 128;
 }
 
+extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_p, uint32_t seed,
+                                       void* mask, smer_stream_t stream) {
+  SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && mask, "smer_attn_drop_mask_gen: bad arguments");
+  SMER_REQUIRE(drop_p > 0.f && drop_p < 1.f, "smer_attn_drop_mask_gen: drop_p");
+  const int nq16 = (Lq + 15) / 16, nkt = (Lk + 63) / 64;
+  const long nwords = (long)B * H * nq16 * nkt * 64;
+  hipLaunchKernelGGL(attn_drop_mask_gen_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_drop_thr16(drop_p), seed,
+                     (uint16_t*)mask);
+  SMER_CHECK_LAUNCH("smer_attn_drop_mask_gen");
+  return SMER_OK;
+}
+
 extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
                              long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
                              long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
-                             float drop_p, uint32_t seed, void* drop_mask,
+                             float drop_p, uint32_t seed, void* drop_mask, int drop_mask_in,
                              smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq >= 0 && Lk > 0 && D > 0, "smer_attn_fwd: bad sizes");
+  SMER_REQUIRE(!drop_mask_in || drop_mask, "smer_attn_fwd: drop_mask_in without a mask");
   SMER_REQUIRE(!drop_mask || (((uintptr_t)drop_mask) & 15) == 0, "smer_attn_fwd: mask alignment");
   SMER_REQUIRE(q && k && v && o && lse, "smer_attn_fwd: null pointer");
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
@@ -1167,9 +1234,9 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
                  "smer_attn_fwd: row strides must be multiples of 8");
-    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
-    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
-    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, s);
+    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
+    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
+    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     SMER_REQUIRE((size_t)Lk * 16 <= 160 * 1024, "smer_attn_fwd(f32): Lk too large");

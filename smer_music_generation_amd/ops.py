@@ -187,10 +187,17 @@ def attn_drop_mask(B, H, Lq, Lk, device):
 
 
 def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale, drop_p=0.0,
-             seed=0, drop_mask=None):
+             seed=0, drop_mask=None, drop_mask_in=False):
+    """drop_mask: keep-bit buffer the forward fills (hashing) for the
+    backward, or, with drop_mask_in, reads (from attn_drop_mask_gen)."""
     call("smer_attn_fwd", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k),
          _p(v), _ld(v), _p(o), _ld(o), _p(lse), _p(kpm), int(causal), float(scale),
-         float(drop_p), int(seed) & 0xFFFFFFFF, _p(drop_mask), _stream())
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(drop_mask), int(bool(drop_mask_in)), _stream())
+
+
+def attn_drop_mask_gen(mask, *, B, H, Lq, Lk, drop_p, seed):
+    call("smer_attn_drop_mask_gen", B, H, Lq, Lk, float(drop_p), int(seed) & 0xFFFFFFFF,
+         _p(mask), _stream())
 
 
 def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, causal=False,

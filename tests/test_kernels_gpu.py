@@ -324,6 +324,20 @@ def test_attention_dropout(dtype, B, H, L, causal):
                    causal=causal, scale=scale, drop_p=p, seed=seed, drop_mask=mask)
         torch.cuda.synchronize()
         assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
+        # forward reading keep bits from the full-occupancy generator ==
+        # forward hashing them itself (same words, same outputs bit for bit)
+        mask3 = O.attn_drop_mask(B, H, L, L, dev)
+        O.attn_drop_mask_gen(mask3, B=B, H=H, Lq=L, Lk=L, drop_p=p, seed=seed)
+        o3 = torch.empty_like(o)
+        lse3 = torch.empty_like(lse)
+        O.attn_fwd(q, k, v, o3, lse3, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal,
+                   scale=scale, drop_p=p, seed=seed, drop_mask=mask3, drop_mask_in=True)
+        dq3, dk3, dv3 = torch.empty_like(dq), torch.empty_like(dk), torch.empty_like(dv)
+        O.attn_bwd(q, k, v, o3, do, lse3, dq3, dk3, dv3, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm,
+                   causal=causal, scale=scale, drop_p=p, seed=seed, drop_mask=mask3)
+        torch.cuda.synchronize()
+        assert torch.equal(o3, o) and torch.equal(lse3, lse)
+        assert torch.equal(dq3, dq) and torch.equal(dk3, dk) and torch.equal(dv3, dv)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
