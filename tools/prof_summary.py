@@ -14,7 +14,8 @@ for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:int(sys.argv[
                                           100 * float(r['TotalDurationNs']) / tot))
 print("total kernel time per step: %.3f ms" % (tot / 1e6 / steps))
 fam = [r for r in rows if r['Name'].replace('void ', '').startswith(
-    ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm_skinny_bf16_kernel"))]
+    ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm64_bf16_kernel",
+     "gemm_skinny_bf16_kernel"))]
 red = [r for r in rows if r['Name'].startswith("splitk_reduce_kernel")]
 if fam:
     calls = sum(int(r['Calls']) for r in fam)
