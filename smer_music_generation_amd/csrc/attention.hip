@@ -85,7 +85,36 @@ __device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
   }
   return r;
 }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16x2 v;
+  v[0] = (bf16)a;
+  v[1] = (bf16)b;
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ bf16x8 words_bf16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return __builtin_bit_cast(bf16x8, u32x4{a, b, c, d});
+}
+// 0 / ~0 from bit `bit` of w (v_bfe_i32): AND-mask for an f32 lane
+__device__ __forceinline__ uint32_t bitmask32(uint32_t w, uint32_t bit) {
+  return (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1u);
+}
+__device__ __forceinline__ float and_f32(float x, uint32_t m) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m);
+}
 }  // namespace
+
+// Attention-dropout keep words (forward publishes, backward reads): 16 bits
+// per (query 16-block q16, key 64-tile t, forward lane (g, c)); bit 4r + mt
+// = keep of (query 16*q16 + c, key 64t + 16mt + 4g + r), i.e. byte r of
+// smer_attn_bits(rowkey(query), quad 16t + 4mt + g).  Built from the SWAR
+// compare words ge_mt (bit 8r + 7 per key): OR_mt ge_mt >> (7 - mt) puts
+// key (mt, r) at bit 8r + mt; folding the four nibbles gives 4r + mt.
+__device__ __forceinline__ uint32_t attn_fold_keep(uint32_t acc) {
+  const uint32_t y = acc | (acc >> 4);
+  return (y & 0xFFu) | ((y >> 8) & 0xFF00u);
+}
 
 // ---------------------------------------------------------------------------
 // bf16 forward
@@ -94,8 +123,11 @@ __device__ __forceinline__ bf16x8 pack_p(const float (&p)[4][4], int ks) {
 // read from LDS once per wave feed QG groups, halving LDS traffic per MFMA
 // at QG = 2 (the forward is otherwise LDS-bandwidth co-limited).
 // MIN: the keep words come precomputed (attn_drop_mask_gen_kernel) instead
-// of being hashed here: the forward is VALU-bound and the hash (two 32-bit
-// multiplies per key pair) is as much VALU work as the softmax itself.
+// of being hashed here (measured: the separate generator costs more than the
+// hashing it saves; kept as a tested building block).
+// Dropout (DROP): per lane and key tile 4 hashes (one per quad of keys),
+// SWAR byte compares, AND masks on the packed bf16 P -- about 20 VALU
+// instructions per 16 scores besides the softmax.
 template <int D, int QG, bool DROP, bool MIN = false>
 __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
                                                      const bf16* __restrict__ q, long ldq,
@@ -122,6 +154,8 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
   const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
+  // SWAR threshold words for smer_attn_ge (drop_thr = thr8)
+  const uint32_t lo4 = (drop_thr & 127u) * 0x01010101u, dsel = drop_thr < 128u ? ~0u : 0u;
 
   bf16x8 qf[QG][C::NS];
 #pragma unroll
@@ -236,46 +270,44 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
           p[mt][r] = fast_exp2(fmaf(st[gq][mt][r], c, -mc));
           l_run[gq] += p[mt][r];
         }
+      // P as bf16 pairs: word [mt][0] = keys (r0, r1), [mt][1] = (r2, r3).
+      // Dropout zeroes dropped pairs' halves with AND masks; the survivors'
+      // 1 / (1 - p) is folded into the final 1 / l.
+      uint32_t pw[4][2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        pw[mt][0] = pack2(p[mt][0], p[mt][1]);
+        pw[mt][1] = pack2(p[mt][2], p[mt][3]);
+      }
       if (DROP && MIN) {
-        // this lane's keep word of (query 16-block, key tile): bit 4mt + r
         const int q16 = (q0w + gq * 16) >> 4;
         const uint32_t mword = min(q16, nq16 - 1) == q16 ? mw[gq] : 0u;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            p[mt][r] = ((mword >> (mt * 4 + r)) & 1u) ? p[mt][r] * drop_scale : 0.f;
+          for (int rp = 0; rp < 2; ++rp)
+            pw[mt][rp] &= (bitmask32(mword, 8 * rp + mt) & 0xFFFFu) |
+                          (bitmask32(mword, 8 * rp + 4 + mt) & 0xFFFF0000u);
       } else if (DROP) {
-        // keys mt*16+4g+{0,1} and {2,3} share one hash; the keep bits are
-        // also published as the 16x16 sub-block's four ballots (see
-        // smer_drop_mask_bytes) so the backward reads instead of re-hashing
-        const uint32_t pb = (uint32_t)(t * (KVB / 2) + 2 * g);
-        uint32_t mword = 0u;
+        // one hash per quad of keys (16mt + 4g .. +3): byte r decides key r
+        const uint32_t quad0 = (uint32_t)(t * (KVB / 4) + g);
+        uint32_t kacc = 0u;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          bool kp[4];
-#pragma unroll
-          for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hb = smer_pair_bits(rowkey[gq], pb + mt * 8 + rp);
-            kp[2 * rp] = (hb & 0xFFFFu) >= drop_thr;
-            kp[2 * rp + 1] = (hb >> 16) >= drop_thr;
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            p[mt][r] = kp[r] ? p[mt][r] * drop_scale : 0.f;
-            mword |= (uint32_t)kp[r] << (mt * 4 + r);
-          }
+          const uint32_t ge = smer_attn_ge(smer_attn_bits(rowkey[gq], quad0 + 4 * mt), lo4, dsel);
+          const uint32_t bm = ge | (ge - (ge >> 7));  // 0xFF per kept byte
+          pw[mt][0] &= __builtin_amdgcn_perm(bm, bm, 0x01010000u);
+          pw[mt][1] &= __builtin_amdgcn_perm(bm, bm, 0x03030202u);
+          kacc |= ge >> (7 - mt);
         }
-        // this lane's 16 keep bits of (query c16 of group gq, key tile t):
-        // word [bh][q16][t][lane], bit 4mt + r = key t*64 + 16mt + 4g + r
         const int q16 = (q0w + gq * 16) >> 4;
         if (drop_mask && q16 < nq16)
           reinterpret_cast<uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane] =
-              (uint16_t)mword;
+              (uint16_t)attn_fold_keep(kacc);
       }
       m_run[gq] = m_new;
-      pf[gq][0] = pack_p(p, 0);
-      pf[gq][1] = pack_p(p, 1);
+      pf[gq][0] = words_bf16x8(pw[0][0], pw[0][1], pw[1][0], pw[1][1]);
+      pf[gq][1] = words_bf16x8(pw[2][0], pw[2][1], pw[3][0], pw[3][1]);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -299,7 +331,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
     float l = l_run[gq] + __shfl_xor(l_run[gq], 16, 64);
     l += __shfl_xor(l, 32, 64);
     if (qi >= Lq) continue;
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const float inv = l > 0.f ? (DROP ? drop_scale : 1.f) / l : 0.f;
     bf16* orow = o + (long)(b * Lq + qi) * ldo + h * D;
 #pragma unroll
     for (int dt = 0; dt < C::NDT; ++dt) {
@@ -423,8 +455,6 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
 #pragma unroll
     for (int gk = 0; gk < KG; ++gk) {
       const int kj = k0w + gk * 16 + c16;
-      const uint32_t kpair = (uint32_t)kj >> 1;
-      const bool khi = kj & 1;
       float pd[4][4], ds[4][4];
       const int k16 = (k0w + gk * 16) >> 4;
 #pragma unroll
@@ -437,18 +467,16 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
         }
         const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
-        // forward's ballots of sub-block (query 16-block, this key 16-block):
-        // ballot r holds (key 4G+r, query c) at bit 16G+c; this lane wants
-        // key c16 = 4(c16>>2) + (c16&3) for queries 4g..4g+3
         // forward lane (G, c) of word [q16][key tile] holds (query c, key
-        // 16*mk + 4G + R) at bit 4mk + R: this lane (key c16 of 16-block
-        // k16, queries 4g..4g+3) reads words 16*(c16>>2) + 4g .. +3
-        uint32_t mbits = 0u;
+        // 16*mk + 4G + R) at bit 4R + mk: this lane (key c16 of 16-block k16,
+        // queries 4g..4g+3 of block mt) reads the words of lanes
+        // 16*(c16>>2) + 4g .. +3 (one 8-B read), bit 4*(c16&3) + (k16&3)
+        uint32_t mlo = 0u, mhi = 0u;
         if constexpr (use_mask) {
-          const int j = (k16 >> 2) - BX * KG, bit = (k16 & 3) * 4 + (c16 & 3);
+          const int j = (k16 >> 2) - BX * KG;
           const uint64_t w = *reinterpret_cast<const uint64_t*>(&s_msk[cur][mt][j][(c16 >> 2) * 16 + 4 * g]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mbits |= (uint32_t)((w >> (16 * r + bit)) & 1ull) << r;
+          mlo = (uint32_t)w;
+          mhi = (uint32_t)(w >> 32);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -457,18 +485,19 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
           float dpv = dpacc[r];
           float pdv = pv;
           if (DROP) {
-            bool keep;
+            uint32_t m;
             if constexpr (use_mask) {
-              keep = (mbits >> r) & 1u;
+              m = bitmask32(r < 2 ? mlo : mhi, 16 * (r & 1) + 4 * (c16 & 3) + (k16 & 3));
             } else {
-              const uint32_t hb = smer_pair_bits(s_rk[cur][mt * 16 + 4 * g + r], kpair);
-              keep = (khi ? (hb >> 16) : (hb & 0xFFFFu)) >= drop_thr;
+              m = smer_attn_keep(s_rk[cur][mt * 16 + 4 * g + r], drop_thr, (uint32_t)kj) ? ~0u : 0u;
             }
-            pdv = keep ? pv * drop_scale : 0.f;
-            dpv = keep ? dpv * drop_scale : 0.f;
+            // dropped P and dP; the survivors' 1 / (1 - p) goes into the dS
+            // fma here and into dV's final write
+            pdv = and_f32(pv, m);
+            dpv = and_f32(dpv, m);
           }
           pd[mt][r] = pdv;
-          ds[mt][r] = pv * (dpv - d4[r]);
+          ds[mt][r] = pv * fmaf(dpv, DROP ? drop_scale : 1.f, -d4[r]);
         }
       }
       pf[gk][0] = pack_p(pd, 0);
@@ -505,7 +534,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         wk[r] = (bf16)(kvalid[gk] ? adk[gk][dt][r] * scale : 0.f);
-        wv[r] = (bf16)(kvalid[gk] ? adv[gk][dt][r] : 0.f);
+        wv[r] = (bf16)(kvalid[gk] ? adv[gk][dt][r] * (DROP ? drop_scale : 1.f) : 0.f);
       }
       *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
       *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
@@ -637,25 +666,21 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) dpv[r] = dpacc[gq][mt][r];
         if constexpr (use_mask) {
-          // same lane mapping as the forward: bit 4mt + r of this lane's word
+          // same lane mapping as the forward: bit 4r + mt of this lane's word
           const uint32_t w = s_msk[cur][((q0w - BX * QB) >> 4) + gq][lane];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            dpv[r] = ((w >> (mt * 4 + r)) & 1u) ? dpv[r] * drop_scale : 0.f;
+          for (int r = 0; r < 4; ++r) dpv[r] = and_f32(dpv[r], bitmask32(w, 4 * r + mt));
         } else if (DROP) {
-          const uint32_t pb = (uint32_t)(t * (KVB / 2) + mt * 8 + 2 * g);
+          const uint32_t hb = smer_attn_bits(rowkey[gq], (uint32_t)(t * (KVB / 4) + mt * 4 + g));
 #pragma unroll
-          for (int rp = 0; rp < 2; ++rp) {
-            const uint32_t hb = smer_pair_bits(rowkey[gq], pb + rp);
-            dpv[2 * rp] = (hb & 0xFFFFu) >= drop_thr ? dpv[2 * rp] * drop_scale : 0.f;
-            dpv[2 * rp + 1] = (hb >> 16) >= drop_thr ? dpv[2 * rp + 1] * drop_scale : 0.f;
-          }
+          for (int r = 0; r < 4; ++r) dpv[r] = ((hb >> (8 * r)) & 0xFFu) >= drop_thr ? dpv[r] : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = fast_exp2(fmaf(sacc[gq][mt][r], c, -lse2[gq]));
           if (diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
-          ds[mt][r] = pv * (dpv[r] - dlt[gq]);
+          // dS = P (keep * dP / (1 - p) - delta)
+          ds[mt][r] = pv * fmaf(dpv[r], DROP ? drop_scale : 1.f, -dlt[gq]);
         }
       }
       sf[gq][0] = pack_p(ds, 0);
@@ -797,7 +822,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int B, int H, int Lq, int Lk
   for (int j = lane; j < Lk; j += 64) {
     float e = expf(sc[j] - mu);
     sum += e;
-    if (drop_thr) e = smer_keep16(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j) ? e * drop_scale : 0.f;
+    if (drop_thr) e = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j) ? e * drop_scale : 0.f;
     sc[j] = e;
   }
   sum = wave_sum(sum);
@@ -838,7 +863,7 @@ __global__ void attn_bwd_ps_f32(int B, int H, int Lq, int Lk, int D, const float
   }
   float pd = p;
   if (drop_thr) {
-    bool keep = smer_keep16(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j);
+    bool keep = smer_attn_keep(smer_rowkey(seed, (uint32_t)(bh * Lq + qi)), drop_thr, (uint32_t)j);
     pd = keep ? p * drop_scale : 0.f;
     dp = keep ? dp * drop_scale : 0.f;
   }
@@ -1144,9 +1169,8 @@ __global__ void kv_scatter_heads_kernel(int n_rows, int H, int D, const T* __res
 }
 
 // The attention-dropout keep words of a whole [B*H, Lq, Lk] score matrix,
-// bit for bit what attn_fwd_bf16 (hashing path) publishes: word [bh][q16][t]
-// [lane (g, c)] holds query 16*q16 + c, key 64t + 16mt + 4g + r at bit
-// 4mt + r (smer_attn_drop_mask_bytes).  Pure integer VALU at full occupancy.
+// bit for bit what attn_fwd_bf16 (hashing path) publishes (layout: see
+// attn_fold_keep).  Pure integer VALU at full occupancy.
 __global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(long nwords, int Lq, int nq16, int nkt,
                                                                 uint32_t thr, uint32_t seed,
                                                                 uint16_t* __restrict__ out) {
@@ -1159,18 +1183,14 @@ __global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(long nwords, in
   const int q16 = (int)(r2 % nq16);
   const long bh = r2 / nq16;
   const int g = lane >> 4, c = lane & 15;
+  const uint32_t lo4 = (thr & 127u) * 0x01010101u, sel = thr < 128u ? ~0u : 0u;
   const uint32_t rowkey = smer_rowkey(seed, (uint32_t)(bh * Lq + q16 * 16 + c));
-  const uint32_t pb = (uint32_t)(t * (KVB / 2) + 2 * g);
-  uint32_t mword = 0u;
+  const uint32_t quad0 = (uint32_t)(t * (KVB / 4) + g);
+  uint32_t acc = 0u;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int rp = 0; rp < 2; ++rp) {
-      const uint32_t hb = smer_pair_bits(rowkey, pb + mt * 8 + rp);
-      mword |= (uint32_t)((hb & 0xFFFFu) >= thr) << (mt * 4 + 2 * rp);
-      mword |= (uint32_t)((hb >> 16) >= thr) << (mt * 4 + 2 * rp + 1);
-    }
-  out[w] = (uint16_t)mword;
+    acc |= smer_attn_ge(smer_attn_bits(rowkey, quad0 + 4 * mt), lo4, sel) >> (7 - mt);
+  out[w] = (uint16_t)attn_fold_keep(acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1198,7 +1218,7 @@ static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
 
 // [bh][query 16-block][key 64-tile][64 lanes] 16-bit words: lane (g, c) of
 // the forward's wave holds (query 16*q16 + c, key 64*t + 16*mt + 4g + r) at
-// bit 4mt + r.  1 bit per (query, key).
+// bit 4r + mt.  1 bit per (query, key).
 extern "C" size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk) {
   return (size_t)B * H * ((Lq + 15) / 16) * ((Lk + 63) / 64) * 128;
 }
@@ -1210,7 +1230,7 @@ extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_
   const int nq16 = (Lq + 15) / 16, nkt = (Lk + 63) / 64;
   const long nwords = (long)B * H * nq16 * nkt * 64;
   hipLaunchKernelGGL(attn_drop_mask_gen_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_drop_thr16(drop_p), seed,
+                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_attn_thr8(drop_p), seed,
                      (uint16_t*)mask);
   SMER_CHECK_LAUNCH("smer_attn_drop_mask_gen");
   return SMER_OK;
@@ -1228,8 +1248,8 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
   if (Lq == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_drop_thr16(drop_p);
-  float ds = smer_drop_scale16(thr);
+  uint32_t thr = smer_attn_thr8(drop_p);
+  float ds = smer_attn_scale8(thr);
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
@@ -1300,8 +1320,8 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
                "smer_attn_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_drop_thr16(drop_p);
-  float ds = smer_drop_scale16(thr);
+  uint32_t thr = smer_attn_thr8(drop_p);
+  float ds = smer_attn_scale8(thr);
   float* delta = (float*)workspace;
   long nrow = (long)B * H * Lq;
   if (dtype == SMER_BF16) {

@@ -85,6 +85,43 @@ static inline float smer_drop_scale16(uint32_t thr16) {
   return thr16 ? (float)(65536.0 / (65536.0 - (double)thr16)) : 1.f;
 }
 
+// Attention-probability dropout: the flash forward spends its VALU budget on
+// the softmax, so this site uses 8-bit keep thresholds (as FlashAttention's
+// uint8 dropout does) and a cheaper mixer.  One 32-bit hash per (query row,
+// quad of 4 consecutive keys); byte r decides key 4*quad + r, kept when
+// byte >= thr8 = round(p * 256) (realised rate thr8 / 256, survivors scaled
+// by 256 / (256 - thr8): unbiased for that rate).  The mixer multiplies with
+// the full-rate 24-bit multiplier (v_mul_u32_u24; the xor-shifts fold the
+// high bits down first).  numpy mirror: tests/hashref.py attn_keep_mask.
+__device__ __forceinline__ uint32_t smer_attn_bits(uint32_t rowkey, uint32_t quad) {
+  uint32_t h = rowkey + quad * 0x9E3779B9u;
+  h ^= h >> 16;
+  h = __umul24(h, 0xEB352Du);
+  h ^= h >> 15;
+  h = __umul24(h, 0x6CA68Bu);
+  h ^= h >> 16;
+  return h;
+}
+// The four byte decisions of one hash at once (SWAR): bit 8r + 7 of the
+// result is set iff byte r >= thr8.  lo4 = (thr8 & 127) * 0x01010101, sel =
+// ~0u when thr8 < 128 (byte >= t <=> top bit | low7 >= t) else 0 (top bit &
+// low7 >= t - 128); no borrow crosses a byte since every minuend byte >= 128.
+__device__ __forceinline__ uint32_t smer_attn_ge(uint32_t h, uint32_t lo4, uint32_t sel) {
+  const uint32_t d = (h | 0x80808080u) - lo4;
+  return ((h & d) | (sel & (h ^ d))) & 0x80808080u;
+}
+__device__ __forceinline__ bool smer_attn_keep(uint32_t rowkey, uint32_t thr8, uint32_t key) {
+  return ((smer_attn_bits(rowkey, key >> 2) >> (8 * (key & 3))) & 0xFFu) >= thr8;
+}
+static inline uint32_t smer_attn_thr8(float p) {
+  if (p <= 0.f) return 0u;
+  long t = (long)((double)p * 256.0 + 0.5);
+  return (uint32_t)(t < 1 ? 1 : (t > 255 ? 255 : t));
+}
+static inline float smer_attn_scale8(uint32_t thr8) {
+  return thr8 ? (float)(256.0 / (256.0 - (double)thr8)) : 1.f;
+}
+
 // out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order
 // (deterministic; two levels when nblk > 64, `scratch` of
 // smer_col_reduce_scratch(nblk, N) bytes).  Defined in train_ops.hip.

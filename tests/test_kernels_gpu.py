@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.hashref import attn_keep_mask, attn_scale, keep_mask
+from tests.hashref import attn_keep_mask, attn_scale, drop_scale, keep_mask
 
 pytestmark = pytest.mark.gpu
 
@@ -122,7 +122,7 @@ def test_gemm256_large_m(M, N, K, bk):
            seed=seed)
     base = A.float() @ W.float().t()
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * drop_scale(p), torch.zeros_like(base))
     Cf = torch.empty(M, N, device=dev)
     O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out_f32=Cf)
     torch.cuda.synchronize()
@@ -179,7 +179,7 @@ def test_gemm_epilogue(dtype, M, N, K):
     C = torch.empty(M, N, device=dev, dtype=dtype)
     O.gemm(A, W, M=M, N=N, K=K, out=C, bias=bias, relu=True, residual=R, drop_p=p, seed=seed)
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * drop_scale(p), torch.zeros_like(base))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < tol
     # gate (relu-backward) + fp32 accumulate
@@ -193,7 +193,7 @@ def test_gemm_epilogue(dtype, M, N, K):
 
 # ------------------------------------------------------------ attention
 def attn_ref(q, k, v, B, H, Lq, Lk, D, kpm, causal, scale, keep=None, p=0.0):
-    """fp32 reference; dropout survivors scaled by the kernel's 16-bit-rate
+    """fp32 reference; dropout survivors scaled by the kernel's 8-bit-rate
     factor (tests/hashref.py attn_scale)."""
     qh = q.float().view(B, Lq, H, D).transpose(1, 2)
     kh = k.float().view(B, Lk, H, D).transpose(1, 2)
@@ -444,7 +444,7 @@ def test_layernorm(dtype, M, N):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     assert rel_err(dx, xf.grad) < tol
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    assert rel_err(dxd, torch.where(keep, xf.grad * attn_scale(p), torch.zeros_like(xf.grad))) < tol
+    assert rel_err(dxd, torch.where(keep, xf.grad * drop_scale(p), torch.zeros_like(xf.grad))) < tol
     assert rel_err(dg, gf.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
     assert rel_err(db, bf.grad) < (1e-2 if dtype == torch.bfloat16 else 1e-5)
 
@@ -464,7 +464,7 @@ def test_embedding(dtype):
     keep = torch.from_numpy(keep_mask(seed, p, B * L, d)).to(dev)
     pos = torch.arange(B * L, device=dev) % L
     ref = table[ids.view(-1)] * math.sqrt(d) + pe[pos]
-    ref = torch.where(keep, ref * attn_scale(p), torch.zeros_like(ref))
+    ref = torch.where(keep, ref * drop_scale(p), torch.zeros_like(ref))
     torch.cuda.synchronize()
     assert rel_err(out, ref) < (1e-2 if dtype == torch.bfloat16 else 1e-6)
     ids2 = torch.randint(0, V, (2, 30), device=dev)
@@ -473,7 +473,7 @@ def test_embedding(dtype):
     dt = torch.zeros(V, d, device=dev)
     O.embed_bwd(dt, math.sqrt(d), [(ids.view(-1), dx0, p, seed), (ids2.view(-1), dx1, 0.0, 0)])
     ref = torch.zeros(V, d, device=dev)
-    g0 = torch.where(keep, dx0.float() * attn_scale(p), torch.zeros_like(dx0.float()))
+    g0 = torch.where(keep, dx0.float() * drop_scale(p), torch.zeros_like(dx0.float()))
     ref.index_add_(0, ids.view(-1), g0)
     ref.index_add_(0, ids2.view(-1), dx1.float())
     ref *= math.sqrt(d)
@@ -540,8 +540,8 @@ def test_adam_and_cast_and_colsum():
 @pytest.mark.parametrize("B,H,Lq,Lk,causal", [(2, 2, 96, 96, True), (2, 2, 80, 150, False),
                                               (16, 8, 512, 512, False)])
 def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
-    """The forward's stored keep bits equal tests/hashref.keep_mask: 16-bit
-    words [bh][q16][key tile t][lane = 16g + c], bit 4mt + r = (query
+    """The forward's stored keep bits equal tests/hashref.attn_keep_mask:
+    16-bit words [bh][q16][key tile t][lane = 16g + c], bit 4r + mt = (query
     16*q16 + c, key 64t + 16mt + 4g + r)."""
     O = ops()
     D, p, seed = 64, 0.1, 99
@@ -556,9 +556,9 @@ def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
     nq, nt = (Lq + 15) // 16, (Lk + 63) // 64
     w = mask[: B * H * nq * nt * 128].cpu().numpy().view(np.uint16).reshape(B * H, nq, nt, 4, 16)
     bits = (w[..., None].astype(np.uint32) >> np.arange(16, dtype=np.uint32)) & 1  # [bh,q16,t,g,c,16]
-    bits = bits.reshape(B * H, nq, nt, 4, 16, 4, 4)                                  # [.., g, c, mt, r]
-    got = bits.transpose(0, 1, 4, 2, 5, 3, 6).reshape(B * H, nq * 16, nt * 64)       # [bh, q, key]
-    ref = keep_mask(seed, p, B * H * Lq, Lk).reshape(B * H, Lq, Lk)
+    bits = bits.reshape(B * H, nq, nt, 4, 16, 4, 4)                                  # [.., g, c, r, mt]
+    got = bits.transpose(0, 1, 4, 2, 6, 3, 5).reshape(B * H, nq * 16, nt * 64)       # [bh, q, key]
+    ref = attn_keep_mask(seed, p, B * H * Lq, Lk).reshape(B * H, Lq, Lk)
     sel = np.ones((Lq, Lk), bool) if not causal else np.tril(np.ones((Lq, Lk), bool))
     g = got[:, :Lq, :Lk].astype(bool)
     assert (g[:, sel] == ref[:, sel]).all()
@@ -659,7 +659,7 @@ def test_gemm64_mid_size_epilogues(M, N, K, bk):
            seed=seed)
     base = A.float() @ W.float().t()
     keep = torch.from_numpy(keep_mask(seed, p, M, N)).to(dev)
-    ref = R.float() + torch.where(keep, torch.relu(base + bias) * attn_scale(p), torch.zeros_like(base))
+    ref = R.float() + torch.where(keep, torch.relu(base + bias) * drop_scale(p), torch.zeros_like(base))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < 2e-2
     O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, gate=R, gate_scale=1.5)
