@@ -139,6 +139,23 @@ def _infill_requests(n, target_len=1024, seed0=0, n_infill_bars=2):
     return reqs
 
 
+def infill_roofline(args, st):
+    """SURVEY.md §8d infill roofline (HBM-bound): every decode step streams
+    the decoder weights (L(6d^2 + 2dF) + dV bf16; the cross K/V projections
+    ran at prefill) and each live request's K/V rows, L * 2d bf16 per key
+    row attended (memory + prefix).  achieved = those bytes / the decode
+    loop's wall time."""
+    L, d, F, V = args.layers, args.d_model, args.ff, 309
+    w_bytes = (L * (6 * d * d + 2 * d * F) + d * V) * 2
+    if not st.get("kv_row_reads") or not st.get("step_call_s"):
+        return None
+    total = st["steps"] * w_bytes + st["kv_row_reads"] * L * 2 * d * 2
+    gbs = total / st["step_call_s"] / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": round(total / max(1, st["steps"])),
+            "weight_bytes_per_step": w_bytes}
+
+
 def bench_infill(args, dev, rank):
     from smer_music_generation_amd.generation import generation_batch
     from smer_music_generation_amd.vocab import WordVocab
@@ -157,7 +174,9 @@ def bench_infill(args, dev, rank):
     return {"tokens": st["tokens"], "steps": st["steps"], "seconds": dt,
             "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s",
                                                       "step_call_s")},
-            "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len}
+            "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len,
+            "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
+            "roofline": infill_roofline(args, st)}
 
 
 def bench_infill_c5(args, dev, rank):
@@ -186,6 +205,7 @@ def bench_infill_c5(args, dev, rank):
             "p50_latency_s": float(np.percentile(lat, 50)),
             "p90_latency_s": float(np.percentile(lat, 90)),
             "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
+            "roofline": infill_roofline(args, st),
             "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s")}}
 
 
@@ -339,6 +359,8 @@ def main():
                                "requests_per_gpu": inf["requests"],
                                "mean_src_len": round(inf["mean_src_len"], 1),
                                "decode_steps": inf["steps"], "tokens": inf["tokens"],
+                               "ms_per_decode_step": round(inf["ms_per_decode_step"], 3),
+                               "roofline": inf["roofline"],
                                "phases_s": inf["phases_s"], "parallelism": "replicas"},
             "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
                                           "S=2048 T=512, bf16",
@@ -357,6 +379,7 @@ def main():
                                  "requests_per_gpu": c5["requests"],
                                  "mean_src_len": round(c5["mean_src_len"], 1),
                                  "decode_steps": c5["steps"], "tokens": c5["tokens"],
+                                 "roofline": c5["roofline"],
                                  "phases_s": c5["phases_s"], "parallelism": "replicas"},
             "cpu_baseline": cpu,
         }

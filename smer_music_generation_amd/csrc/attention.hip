@@ -103,6 +103,20 @@ __device__ __forceinline__ uint32_t bitmask32(uint32_t w, uint32_t bit) {
 __device__ __forceinline__ float and_f32(float x, uint32_t m) {
   return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m);
 }
+// max over the four 16-lane groups holding one query's keys (lanes c,
+// c+16, c+32, c+48): two half / row swaps (v_permlane32/16_swap) instead of
+// LDS-routed shuffles; raw v_max (the operands are never NaN)
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float max_4groups(float x) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = vmax_raw(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 }  // namespace
 
 // Attention-dropout keep words (forward publishes, backward reads): 16 bits
@@ -239,19 +253,20 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
       const int qi = q0w + gq * 16 + c16;
       // max in raw score units (c > 0), exponent as one fma: p = 2^(s*c - m*c)
       if (causal && t * KVB + KVB - 1 > q0w + gq * 16) {
+        // key - query = kq0 + 16mt + r: one difference, immediate offsets
+        const int kq0 = t * KVB + 4 * g - qi;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (t * KVB + mt * 16 + 4 * g + r > qi) st[gq][mt][r] = -INFINITY;
+            if (kq0 > -(mt * 16 + r)) st[gq][mt][r] = -INFINITY;
       }
       float tmax = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, st[gq][mt][r]);
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = max_4groups(tmax);
       const float m_new = fmaxf(m_run[gq], tmax);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       // lazy rescale: skip the accumulator multiply while no lane's max moved
@@ -349,7 +364,9 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
 // ---------------------------------------------------------------------------
 // KG key groups of 16 per wave (block = 64*KG keys): the Q / dO fragments
 // read from LDS per query tile feed KG groups.
-template <int D, bool DROP, int KG, bool MSK = false>
+// CAUSAL: the causal instances carry the per-element key > query test on
+// diagonal tiles; the non-causal ones (encoder, cross-attention) none.
+template <int D, bool DROP, int KG, bool MSK, bool CAUSAL>
 __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
@@ -413,6 +430,11 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   uint4 rm = make_uint4(0, 0, 0, 0);
   constexpr int MCH = KG * 128 / 16;  // 16-B chunks per query 16-block row
   constexpr bool use_mask = DROP && MSK;
+  // this thread's mask chunk: query 16-block t*4 + m_qr, key tile m_kt
+  const int m_qr = tid / MCH, m_ch = tid % MCH, m_kt = BX * KG + m_ch / 8;
+  const uint4* m_base = use_mask ? reinterpret_cast<const uint4*>(drop_mask) +
+                                       ((long)bh * nq16 * nkt + m_kt) * 8 + (m_ch & 7)
+                                 : nullptr;
   auto load = [&](int t) {
     tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
     tile_load<D>(ro, ob, lddo, t * KVB, Lq, tid);
@@ -423,11 +445,8 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       if (DROP && !MSK) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
     }
     if (use_mask && tid < 4 * MCH) {
-      const int qr = tid / MCH, ch = tid % MCH;
-      const int q16 = t * 4 + qr, kt = BX * KG + ch / 8;
-      rm = (q16 < nq16 && kt < nkt)
-               ? reinterpret_cast<const uint4*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + kt) * 8 + (ch & 7)]
-               : make_uint4(0, 0, 0, 0);
+      const int q16 = t * 4 + m_qr;
+      rm = (q16 < nq16 && m_kt < nkt) ? m_base[q16 * nkt * 8] : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&](int buf) {
@@ -450,7 +469,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     const char* Qs = sm[cur][0];
     const char* Os = sm[cur][1];
     // some key of this wave is later than some query of the tile
-    const bool diag = causal && t * KVB < k0w + 16 * KG;
+    const bool diag = CAUSAL && t * KVB < k0w + 16 * KG;
     bf16x8 pf[KG][2], sf[KG][2];
 #pragma unroll
     for (int gk = 0; gk < KG; ++gk) {
@@ -481,7 +500,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = fast_exp2(fmaf(sacc[r], c, -l4[r]));
-          if (diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
+          if (CAUSAL && diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
           float dpv = dpacc[r];
           float pdv = pv;
           if (DROP) {
@@ -545,7 +564,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
 // ---------------------------------------------------------------------------
 // bf16 backward: dQ
 // ---------------------------------------------------------------------------
-template <int D, bool DROP, int QG, bool MSK = false>
+template <int D, bool DROP, int QG, bool MSK, bool CAUSAL>
 __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
@@ -570,12 +589,12 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   const float c = scale * LOG2E_F;
   constexpr bool use_mask = DROP && MSK;
   // 16-B chunk `ch` of the block's mask words for key tile t (8 per q16)
+  const int m_q16 = (BX * QB >> 4) + (tid >> 3);
+  const uint4* m_base = use_mask ? reinterpret_cast<const uint4*>(drop_mask) +
+                                       ((long)bh * nq16 + m_q16) * nkt * 8 + (tid & 7)
+                                 : nullptr;
   auto mask_load = [&](int t, int ch) -> uint4 {
-    const int qr = ch >> 3, cc = ch & 7;
-    const int q16 = (BX * QB >> 4) + qr;
-    return q16 < nq16
-               ? reinterpret_cast<const uint4*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 8 + cc]
-               : make_uint4(0, 0, 0, 0);
+    return m_q16 < nq16 ? m_base[t * 8] : make_uint4(0, 0, 0, 0);
   };
   bf16x8 qf[QG][C::NS], of[QG][C::NS];
   float lse2[QG], dlt[QG];
@@ -658,7 +677,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
 #pragma unroll
     for (int gq = 0; gq < QG; ++gq) {
       const int qi = q0w + gq * 16 + c16;
-      const bool diag = causal && t * KVB + KVB - 1 > q0w + gq * 16;
+      const bool diag = CAUSAL && t * KVB + KVB - 1 > q0w + gq * 16;
       float ds[4][4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
@@ -678,7 +697,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = fast_exp2(fmaf(sacc[gq][mt][r], c, -lse2[gq]));
-          if (diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
+          if (CAUSAL && diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
           // dS = P (keep * dP / (1 - p) - delta)
           ds[mt][r] = pv * fmaf(dpv[r], DROP ? drop_scale : 1.f, -dlt[gq]);
         }
@@ -1288,16 +1307,16 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
   // two key groups per wave once there are enough blocks to fill the chip
   const bool kg2 = (long)((Lk + 127) / 128) * B * H >= 512 && D <= 64;
   // dropout variants: recompute the keep bits by hashing, or read the
-  // forward's stored bits (MSK)
-  auto kdkdv = kg2 ? (!thr ? attn_bwd_dkdv_bf16<D, false, 2>
-                      : mask ? attn_bwd_dkdv_bf16<D, true, 2, true> : attn_bwd_dkdv_bf16<D, true, 2>)
-                   : (!thr ? attn_bwd_dkdv_bf16<D, false, 1>
-                      : mask ? attn_bwd_dkdv_bf16<D, true, 1, true> : attn_bwd_dkdv_bf16<D, true, 1>);
+  // forward's stored bits (MSK); causal and non-causal instances
+#define SMER_BWD_PICK(K, G, C)                                                        \
+  (!thr ? K<D, false, G, false, C> : mask ? K<D, true, G, true, C> : K<D, true, G, false, C>)
+  const bool cz = causal != 0;
+  auto kdkdv = kg2 ? (cz ? SMER_BWD_PICK(attn_bwd_dkdv_bf16, 2, true) : SMER_BWD_PICK(attn_bwd_dkdv_bf16, 2, false))
+                   : (cz ? SMER_BWD_PICK(attn_bwd_dkdv_bf16, 1, true) : SMER_BWD_PICK(attn_bwd_dkdv_bf16, 1, false));
   const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
-  auto kdq = qg2 ? (!thr ? attn_bwd_dq_bf16<D, false, 2>
-                    : mask ? attn_bwd_dq_bf16<D, true, 2, true> : attn_bwd_dq_bf16<D, true, 2>)
-                 : (!thr ? attn_bwd_dq_bf16<D, false, 1>
-                    : mask ? attn_bwd_dq_bf16<D, true, 1, true> : attn_bwd_dq_bf16<D, true, 1>);
+  auto kdq = qg2 ? (cz ? SMER_BWD_PICK(attn_bwd_dq_bf16, 2, true) : SMER_BWD_PICK(attn_bwd_dq_bf16, 2, false))
+                 : (cz ? SMER_BWD_PICK(attn_bwd_dq_bf16, 1, true) : SMER_BWD_PICK(attn_bwd_dq_bf16, 1, false));
+#undef SMER_BWD_PICK
   hipLaunchKernelGGL(kdkdv, dim3(kg2 ? (Lk + 127) / 128 : (Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,

@@ -405,6 +405,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         t_dev = 0.0
         fed = [0] * R
         latency = None
+        kv_reads = None
         if greedy and device_grammar:
             keep, cls = grammar_tables(vocab, all_controls)
             m0 = vocab.char2index('m_0')
@@ -417,6 +418,10 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
             latency = [(ts - t0) + (step_ms[len(q) - 1] / 1000.0 if q else 0.0) for q in seqs]
             if np.any(err):
                 raise ValueError("decoder prefix exceeds session max_tgt %d" % (sess.Tmax - 1))
+            # key rows the decode steps attended to (SURVEY §8d infill bytes):
+            # request r's i-th step reads its S_r memory rows and i+1 prefix rows
+            kv_reads = int(sum(len(q) * len(p[0]) + len(q) * (len(q) + 1) // 2
+                               for q, p in zip(seqs, preps)))
             for sp, seq in zip(spans, seqs):
                 for idx in seq:
                     _, chk, msg = sp.spec()
@@ -460,5 +465,5 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         t3 = time.perf_counter()
         return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,
                      "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev,
-                     "request_latency_s": latency}
+                     "request_latency_s": latency, "kv_row_reads": kv_reads}
     return out
