@@ -96,6 +96,11 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 __device__ __forceinline__ bf16x8 words_bf16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return __builtin_bit_cast(bf16x8, u32x4{a, b, c, d});
 }
+// each 16-bit half -> 0xFFFF if its top bit is set, else 0 (v_pk_ashrrev_i16)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t half_masks(uint32_t x) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, x) >> (short)15);
+}
 // 0 / ~0 from bit `bit` of w (v_bfe_i32): AND-mask for an f32 lane
 __device__ __forceinline__ uint32_t bitmask32(uint32_t w, uint32_t bit) {
   return (uint32_t)__builtin_amdgcn_sbfe((int)w, bit, 1u);
@@ -143,7 +148,7 @@ __device__ __forceinline__ uint32_t attn_fold_keep(uint32_t acc) {
 // SWAR byte compares, AND masks on the packed bf16 P -- about 20 VALU
 // instructions per 16 scores besides the softmax.
 template <int D, int QG, bool DROP, bool MIN = false>
-__global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
+__global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
                                                      const bf16* __restrict__ q, long ldq,
                                                      const bf16* __restrict__ k, long ldk,
                                                      const bf16* __restrict__ v, long ldv,
@@ -168,8 +173,8 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
   const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
-  // SWAR threshold words for smer_attn_ge (drop_thr = thr8)
-  const uint32_t lo4 = (drop_thr & 127u) * 0x01010101u, dsel = drop_thr < 128u ? ~0u : 0u;
+  // SWAR threshold word for smer_attn_ge (drop_thr = thr7)
+  const uint32_t lo4 = drop_thr * 0x01010101u;
 
   bf16x8 qf[QG][C::NS];
 #pragma unroll
@@ -309,11 +314,12 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_fwd_bf16(int B, int
         uint32_t kacc = 0u;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          const uint32_t ge = smer_attn_ge(smer_attn_bits(rowkey[gq], quad0 + 4 * mt), lo4, dsel);
-          const uint32_t bm = ge | (ge - (ge >> 7));  // 0xFF per kept byte
-          pw[mt][0] &= __builtin_amdgcn_perm(bm, bm, 0x01010000u);
-          pw[mt][1] &= __builtin_amdgcn_perm(bm, bm, 0x03030202u);
-          kacc |= ge >> (7 - mt);
+          const uint32_t ge = smer_attn_ge(smer_attn_bits(rowkey[gq], quad0 + 4 * mt), lo4);
+          // bytes [r0 r0 r1 r1] / [r2 r2 r3 r3], then each 16-bit half's
+          // sign (the keep bit) smeared over the half
+          pw[mt][0] &= half_masks(__builtin_amdgcn_perm(ge, ge, 0x01010000u));
+          pw[mt][1] &= half_masks(__builtin_amdgcn_perm(ge, ge, 0x03030202u));
+          kacc |= (ge >> (7 - mt)) & (0x01010101u << mt);
         }
         const int q16 = (q0w + gq * 16) >> 4;
         if (drop_mask && q16 < nq16)
@@ -692,7 +698,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
         } else if (DROP) {
           const uint32_t hb = smer_attn_bits(rowkey[gq], (uint32_t)(t * (KVB / 4) + mt * 4 + g));
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dpv[r] = ((hb >> (8 * r)) & 0xFFu) >= drop_thr ? dpv[r] : 0.f;
+          for (int r = 0; r < 4; ++r) dpv[r] = ((hb >> (8 * r)) & 0x7Fu) >= drop_thr ? dpv[r] : 0.f;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1202,13 +1208,13 @@ __global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(long nwords, in
   const int q16 = (int)(r2 % nq16);
   const long bh = r2 / nq16;
   const int g = lane >> 4, c = lane & 15;
-  const uint32_t lo4 = (thr & 127u) * 0x01010101u, sel = thr < 128u ? ~0u : 0u;
+  const uint32_t lo4 = thr * 0x01010101u;
   const uint32_t rowkey = smer_rowkey(seed, (uint32_t)(bh * Lq + q16 * 16 + c));
   const uint32_t quad0 = (uint32_t)(t * (KVB / 4) + g);
   uint32_t acc = 0u;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
-    acc |= smer_attn_ge(smer_attn_bits(rowkey, quad0 + 4 * mt), lo4, sel) >> (7 - mt);
+    acc |= (smer_attn_ge(smer_attn_bits(rowkey, quad0 + 4 * mt), lo4) >> (7 - mt)) & (0x01010101u << mt);
   out[w] = (uint16_t)attn_fold_keep(acc);
 }
 
@@ -1249,7 +1255,7 @@ extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_
   const int nq16 = (Lq + 15) / 16, nkt = (Lk + 63) / 64;
   const long nwords = (long)B * H * nq16 * nkt * 64;
   hipLaunchKernelGGL(attn_drop_mask_gen_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_attn_thr8(drop_p), seed,
+                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_attn_thr7(drop_p), seed,
                      (uint16_t*)mask);
   SMER_CHECK_LAUNCH("smer_attn_drop_mask_gen");
   return SMER_OK;
@@ -1267,8 +1273,8 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_attn_fwd: drop_p");
   if (Lq == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_attn_thr8(drop_p);
-  float ds = smer_attn_scale8(thr);
+  uint32_t thr = smer_attn_thr7(drop_p);
+  float ds = smer_attn_scale7(thr);
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
@@ -1339,8 +1345,8 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
                "smer_attn_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
-  uint32_t thr = smer_attn_thr8(drop_p);
-  float ds = smer_attn_scale8(thr);
+  uint32_t thr = smer_attn_thr7(drop_p);
+  float ds = smer_attn_scale7(thr);
   float* delta = (float*)workspace;
   long nrow = (long)B * H * Lq;
   if (dtype == SMER_BF16) {

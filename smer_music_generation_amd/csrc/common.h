@@ -86,13 +86,14 @@ static inline float smer_drop_scale16(uint32_t thr16) {
 }
 
 // Attention-probability dropout: the flash forward spends its VALU budget on
-// the softmax, so this site uses 8-bit keep thresholds (as FlashAttention's
-// uint8 dropout does) and a cheaper mixer.  One 32-bit hash per (query row,
-// quad of 4 consecutive keys); byte r decides key 4*quad + r, kept when
-// byte >= thr8 = round(p * 256) (realised rate thr8 / 256, survivors scaled
-// by 256 / (256 - thr8): unbiased for that rate).  The mixer multiplies with
-// the full-rate 24-bit multiplier (v_mul_u32_u24; the xor-shifts fold the
-// high bits down first).  numpy mirror: tests/hashref.py attn_keep_mask.
+// the softmax, so this site uses 7-bit keep thresholds (FlashAttention's
+// uint8 dropout quantises p the same way) and a cheaper mixer.  One 32-bit
+// hash per (query row, quad of 4 consecutive keys); the low 7 bits of byte r
+// decide key 4*quad + r, kept when they are >= thr7 = round(p * 128)
+// (realised rate thr7 / 128, survivors scaled by 128 / (128 - thr7):
+// unbiased for that rate).  The mixer multiplies with the full-rate 24-bit
+// multiplier (v_mul_u32_u24; the xor-shifts fold the high bits down first).
+// numpy mirror: tests/hashref.py attn_keep_mask.
 __device__ __forceinline__ uint32_t smer_attn_bits(uint32_t rowkey, uint32_t quad) {
   uint32_t h = rowkey + quad * 0x9E3779B9u;
   h ^= h >> 16;
@@ -103,23 +104,22 @@ __device__ __forceinline__ uint32_t smer_attn_bits(uint32_t rowkey, uint32_t qua
   return h;
 }
 // The four byte decisions of one hash at once (SWAR): bit 8r + 7 of the
-// result is set iff byte r >= thr8.  lo4 = (thr8 & 127) * 0x01010101, sel =
-// ~0u when thr8 < 128 (byte >= t <=> top bit | low7 >= t) else 0 (top bit &
-// low7 >= t - 128); no borrow crosses a byte since every minuend byte >= 128.
-__device__ __forceinline__ uint32_t smer_attn_ge(uint32_t h, uint32_t lo4, uint32_t sel) {
-  const uint32_t d = (h | 0x80808080u) - lo4;
-  return ((h & d) | (sel & (h ^ d))) & 0x80808080u;
+// result is set iff (byte r & 127) >= thr7; lo4 = thr7 * 0x01010101.  Every
+// minuend byte is >= 128 > thr7, so no borrow crosses a byte; the other
+// bits of the result are don't-care.
+__device__ __forceinline__ uint32_t smer_attn_ge(uint32_t h, uint32_t lo4) {
+  return (h | 0x80808080u) - lo4;
 }
-__device__ __forceinline__ bool smer_attn_keep(uint32_t rowkey, uint32_t thr8, uint32_t key) {
-  return ((smer_attn_bits(rowkey, key >> 2) >> (8 * (key & 3))) & 0xFFu) >= thr8;
+__device__ __forceinline__ bool smer_attn_keep(uint32_t rowkey, uint32_t thr7, uint32_t key) {
+  return ((smer_attn_bits(rowkey, key >> 2) >> (8 * (key & 3))) & 0x7Fu) >= thr7;
 }
-static inline uint32_t smer_attn_thr8(float p) {
+static inline uint32_t smer_attn_thr7(float p) {
   if (p <= 0.f) return 0u;
-  long t = (long)((double)p * 256.0 + 0.5);
-  return (uint32_t)(t < 1 ? 1 : (t > 255 ? 255 : t));
+  long t = (long)((double)p * 128.0 + 0.5);
+  return (uint32_t)(t < 1 ? 1 : (t > 127 ? 127 : t));
 }
-static inline float smer_attn_scale8(uint32_t thr8) {
-  return thr8 ? (float)(256.0 / (256.0 - (double)thr8)) : 1.f;
+static inline float smer_attn_scale7(uint32_t thr7) {
+  return thr7 ? (float)(128.0 / (128.0 - (double)thr7)) : 1.f;
 }
 
 // out[col] (+)= scale * sum_b part[b*stride + off + col], b in fixed order

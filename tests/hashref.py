@@ -43,7 +43,7 @@ def keep_mask(seed, p, rows, cols, row_ids=None):
     return bits >= np.uint32(drop_threshold(p))
 
 
-# ---- attention probabilities: 8-bit thresholds, one hash per 4 keys ----
+# ---- attention probabilities: 7-bit thresholds, one hash per 4 keys ----
 def mix24(h):
     """csrc/common.h smer_attn_bits' mixer: 24-bit multiplies (v_mul_u32_u24)."""
     with np.errstate(over="ignore"):
@@ -59,21 +59,21 @@ def mix24(h):
 def attn_threshold(p):
     if p <= 0:
         return 0
-    return int(min(255, max(1, int(p * 256.0 + 0.5))))
+    return int(min(127, max(1, int(p * 128.0 + 0.5))))
 
 
 def attn_scale(p):
     t = attn_threshold(p)
-    return 256.0 / (256.0 - t) if t else 1.0
+    return 128.0 / (128.0 - t) if t else 1.0
 
 
 def attn_keep_mask(seed, p, rows, cols, row_ids=None):
     """bool [rows, cols] keep-mask of attention dropout (smer_attn_keep):
-    rows = (b*H + h)*Lq + query, cols = keys; byte (key & 3) of the hash of
-    (row key, key >> 2) is compared with round(p * 256)."""
+    rows = (b*H + h)*Lq + query, cols = keys; the low 7 bits of byte (key & 3)
+    of the hash of (row key, key >> 2) are compared with round(p * 128)."""
     with np.errstate(over="ignore"):
         rk = _rowkeys(seed, rows, row_ids)
         c = np.arange(cols, dtype=np.uint32)
         h = mix24((rk[:, None] + (c[None, :] >> np.uint32(2)) * np.uint32(0x9E3779B9)).astype(np.uint32))
-    byte = (h >> (np.uint32(8) * (c[None, :] & np.uint32(3)))) & np.uint32(0xFF)
+    byte = (h >> (np.uint32(8) * (c[None, :] & np.uint32(3)))) & np.uint32(0x7F)
     return byte >= np.uint32(attn_threshold(p))
