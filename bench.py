@@ -253,6 +253,7 @@ def _pmc_traffic():
     s = json.load(open(files[-1]))
     # the smer_gemm family: 128x128 and 256x256 tile kernels, skinny kernel,
     # split-K slab reduction (one smer_gemm call = tile kernel [+ reduce])
+    s = {(k[5:] if k.startswith("void ") else k): v for k, v in s.items()}
     g = [v for k, v in s.items() if k.startswith(("gemm_bf16_kernel", "gemm256_bf16_kernel",
                                                     "gemm64_bf16_kernel", "gemm_skinny_bf16_kernel"))]
     n = sum(v["launches"] for v in g)
