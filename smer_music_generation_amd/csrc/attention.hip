@@ -1046,7 +1046,7 @@ template <typename T>
 __device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) {
   cvt16b<T>(*reinterpret_cast<const uint4*>(p), v);
 }
-template <typename T, int LPK, int UNR, int NW>
+template <typename T, int LPK, int UNR, int NW, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
     long row_stride, long req_stride, long head_stride, const int32_t* __restrict__ row_req,
@@ -1067,8 +1067,8 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   float m = -INFINITY, l = 0.f, acc[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
-  for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
-    uint4 kr[UNR], vr[UNR];
+  // the K / V rows of key step j0 (UNR keys per lane group)
+  auto load_step = [&](int j0, uint4 (&kr)[UNR], uint4 (&vr)[UNR]) {
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int j = j0 + u * KPB + grp;
@@ -1083,6 +1083,19 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
         kr[u] = *reinterpret_cast<const uint4*>(kc + off);
         vr[u] = *reinterpret_cast<const uint4*>(vc + off);
       }
+    }
+  };
+  // PIPE (memories of >= 2048 keys): the next step's loads are issued
+  // before this step's math (two steps of K / V in flight per lane group;
+  // measured 5.2 -> 5.7 TB/s at 4096 keys, slower at 1000)
+  uint4 kr[UNR], vr[UNR];
+  if (PIPE && nk > 0) load_step(0, kr, vr);
+  for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
+    uint4 kn[UNR], vn[UNR];
+    if constexpr (PIPE) {
+      if (j0 + KPB * UNR < nk) load_step(j0 + KPB * UNR, kn, vn);
+    } else {
+      load_step(j0, kr, vr);
     }
     float sc[UNR];
     float mx = m;
@@ -1113,6 +1126,13 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
         for (int i = 0; i < VEC; ++i) acc[i] = fmaf(p, vv[i], acc[i]);
       }
       m = mx;
+    }
+    if constexpr (PIPE) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        kr[u] = kn[u];
+        vr[u] = vn[u];
+      }
     }
   }
   // merge the groups of a wave (lanes with equal `sub`)
@@ -1426,9 +1446,13 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
     // 4 steps of loads in flight per block, short self-attention caches 4 x 2
     const long cap_rows = head_stride != D ? head_stride / (row_stride > 0 ? row_stride : 1)
                                            : req_stride / (row_stride > 0 ? row_stride : 1);
-    const bool big = cap_rows >= 512;
+    const bool big = cap_rows >= 512, pipe = cap_rows >= 2048;
 #define SMER_DEC_VEC(T, L)                                                                        \
-  if (big)                                                                                        \
+  if (pipe)                                                                                       \
+    hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8, true>), grid, dim3(512), 0, s,         \
+                       (const T*)q, ldq, (const T*)kcache, (const T*)vcache, row_stride,          \
+                       req_stride, head_stride, row_req, row_nkeys, (T*)o, ldo, scale);           \
+  else if (big)                                                                                   \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8>), grid, dim3(512), 0, s, (const T*)q,  \
                        ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride,            \
                        head_stride, row_req, row_nkeys, (T*)o, ldo, scale);                       \
