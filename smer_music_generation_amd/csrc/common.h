@@ -34,15 +34,34 @@ template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf
 // exponents are <= 0 so the fix-up libm's exp2f adds is dead weight.
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Wave-wide all-reduce without LDS round trips: DPP butterflies inside each
+// 16-lane row (quad_perm xor 1 / xor 2, half-mirror, mirror), then the row
+// and half exchanges of v_permlane16/32_swap.  Every lane adds the same
+// pairs (commutative), so all 64 lanes hold bit-identical totals.
+__device__ __forceinline__ float dpp_f(float v, int ctrl) {
+  switch (ctrl) {  // the control must be an immediate
+    case 0xB1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+    case 0x141: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  }
+}
+template <typename OP>
+__device__ __forceinline__ float wave_reduce(float v, OP op) {
+  v = op(v, dpp_f(v, 0xB1));   // lane ^ 1
+  v = op(v, dpp_f(v, 0x4E));   // lane ^ 2
+  v = op(v, dpp_f(v, 0x141));  // 7 - lane within 8
+  v = op(v, dpp_f(v, 0x140));  // 15 - lane within 16
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float x, float y) { return x + y; });
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float x, float y) { return fmaxf(x, y); });
 }
 
 // Dropout (every site: activations, attention probabilities, LN / embedding
