@@ -1046,6 +1046,17 @@ template <typename T>
 __device__ __forceinline__ void load16b(const T* p, float (&v)[16 / sizeof(T)]) {
   cvt16b<T>(*reinterpret_cast<const uint4*>(p), v);
 }
+// Sum over aligned groups of G (4, 8 or 16) lanes by DPP butterflies (no
+// LDS round trip): quad xor 1 / xor 2, then half-mirror (8), mirror (16).
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  v += dpp_f(v, 0xB1);
+  v += dpp_f(v, 0x4E);
+  if constexpr (G >= 8) v += dpp_f(v, 0x141);
+  if constexpr (G >= 16) v += dpp_f(v, 0x140);
+  return v;
+}
+
 template <typename T, int LPK, int UNR, int NW, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
@@ -1106,8 +1117,7 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) s = fmaf(qv[i], kv[i], s);
-#pragma unroll
-      for (int w = 1; w < LPK; w <<= 1) s += __shfl_xor(s, w, 64);
+      s = group_sum<LPK>(s);
       sc[u] = (j0 + u * KPB + grp) < nk ? s : -INFINITY;
       mx = fmaxf(mx, sc[u]);
     }
