@@ -839,56 +839,61 @@ __device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int co
 // per lane per fragment); the NW partial tiles are summed through LDS in
 // fixed order (deterministic), then the epilogue runs on 8-column vectors
 // with its bias / residual already in registers.
-template <int NW, int UNR>
+// MI: 16-row fragments per workgroup (BM = 16 * MI rows).  A workgroup
+// streams its BM rows of A and 16 rows of W over all of K, so its load time
+// grows with (BM + 16) * K: MI = 1 quarters the A bytes per workgroup of
+// the 64-row strip (4x the workgroups, each re-reading its W strip).
+template <int NW, int UNR, int MI = 4>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny_bf16_kernel(int M, int N, int K,
                                                                    const bf16* __restrict__ A, long lda,
                                                                    const bf16* __restrict__ B, long ldb,
                                                                    GemmEpi e) {
-  __shared__ float red[NW][SK_BM][SK_BN + 1];
+  constexpr int BM = 16 * MI;
+  __shared__ float red[NW][BM][SK_BN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * SK_BN, m0 = blockIdx.y * SK_BM;
+  const int n0 = blockIdx.x * SK_BN, m0 = blockIdx.y * BM;
   const int r16 = lane & 15, kq = (lane >> 4) * 8;
   const int ncol = n0 + r16;
   const bool colok = ncol < N;
   // epilogue chunk of this thread (tid < 128: row tid/2, 8 columns)
   const int erow = m0 + (tid >> 1), ecol = n0 + (tid & 1) * 8;
-  const bool eth = tid < SK_BM * 2;
+  const bool eth = tid < BM * 2;
   const bool pre = eth && epi_pre_ok(e, M, N, erow, ecol);
   EpiPre ep;
   if (pre) epi_prefetch(e, erow, ecol, ep);
   const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
-  const bf16* ap[4];
-  bool rowok[4];
+  const bf16* ap[MI];
+  bool rowok[MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < MI; ++i) {
     const int row = m0 + i * 16 + r16;
     rowok[i] = row < M;
     ap[i] = A + (long)(rowok[i] ? row : 0) * lda + kq;
   }
-  f32x4 acc[4];
+  f32x4 acc[MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < MI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nsteps = (K + 31) / 32;
   for (int s0 = wave; s0 < nsteps; s0 += NW * UNR) {
-    bf16x8 a[UNR][4], b[UNR];
+    bf16x8 a[UNR][MI], b[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int k = (s0 + u * NW) * 32;
       const bool kok = k + kq < K;  // K % 8 == 0: a lane's 8-chunk is all in or all out
       b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
         a[u][i] = (rowok[i] && kok) ? *reinterpret_cast<const bf16x8*>(ap[i] + k) : bf16x8{};
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
+      for (int i = 0; i < MI; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
   }
   // D[row 4g+r][col c16] of each 16x16 tile
   const int g = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][i * 16 + 4 * g + r][r16] = acc[i][r];
   __syncthreads();
@@ -1051,6 +1056,16 @@ static int smer_splitk_depth() {
   return v;
 }
 
+// 16-row decode Linear workgroups (SMER_SKINNY16=0: 64-row strips; A/B runs)
+static bool smer_skinny16_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_SKINNY16");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -1072,8 +1087,22 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                         const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s,
                         float* rowsum = nullptr) {
   if (AK && BKC && M <= 4 * SK_BM && !rowsum) {
-    const dim3 grid((N + SK_BN - 1) / SK_BN, (M + SK_BM - 1) / SK_BM);
     const int nsteps = (K + 31) / 32;
+    const int ntn = (N + SK_BN - 1) / SK_BN;
+    // 16-row workgroups while that keeps the grid within two per CU
+    // (per-workgroup load time, not the grid, bounds a decode Linear)
+    const bool m16 = smer_skinny16_enabled() && (long)ntn * ((M + 15) / 16) <= 2L * smer_num_cus();
+    if (m16) {
+      const dim3 grid(ntn, (M + 15) / 16);
+      if (nsteps > 16)
+        hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 4, 1>), grid, dim3(512), 0, s, M, N, K,
+                           (const bf16*)A, lda, (const bf16*)B, ldb, e);
+      else
+        hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 2, 1>), grid, dim3(512), 0, s, M, N, K,
+                           (const bf16*)A, lda, (const bf16*)B, ldb, e);
+      return;
+    }
+    const dim3 grid(ntn, (M + SK_BM - 1) / SK_BM);
     if (nsteps > 16)  // 8 waves x 4 steps (16 waves would spill at 128 VGPRs)
       hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 4>), grid, dim3(512), 0, s, M, N, K,
                          (const bf16*)A, lda, (const bf16*)B, ldb, e);
