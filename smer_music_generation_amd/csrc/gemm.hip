@@ -1066,6 +1066,15 @@ static bool smer_skinny16_enabled() {
   return v == 1;
 }
 
+static long smer_skinny16_cap() {  // workgroups per CU (SMER_SKINNY16_CAP; A/B runs)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_SKINNY16_CAP");
+    v = e ? std::max(1, atoi(e)) : 2;
+  }
+  return v;
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -1091,7 +1100,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     const int ntn = (N + SK_BN - 1) / SK_BN;
     // 16-row workgroups while that keeps the grid within two per CU
     // (per-workgroup load time, not the grid, bounds a decode Linear)
-    const bool m16 = smer_skinny16_enabled() && (long)ntn * ((M + 15) / 16) <= 2L * smer_num_cus();
+    const bool m16 = smer_skinny16_enabled() && (long)ntn * ((M + 15) / 16) <= smer_skinny16_cap() * smer_num_cus();
     if (m16) {
       const dim3 grid(ntn, (M + 15) / 16);
       if (nsteps > 16)

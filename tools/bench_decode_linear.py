@@ -39,7 +39,7 @@ def timeit(fn, iters=50, reps=10):
 
 bf = torch.bfloat16
 shapes = [(64, n, k) for n, k in ((1536, 512), (512, 512), (2048, 512), (512, 2048), (309, 512))]
-shapes += [(128, 512, 2048)]
+shapes += [(128, n, k) for n, k in ((1536, 512), (512, 512), (2048, 512), (512, 2048), (309, 512))]
 if len(sys.argv) > 1 and sys.argv[1] == "sweep":
     shapes = [(64, n, k) for n in (64, 512, 2048) for k in (512, 1024, 2048, 4096)]
 for M, N, K in shapes:
