@@ -24,7 +24,8 @@ N_TRACK_CONTROLS = 3  # density, occupation, polyphony (generation.py:249)
 
 
 def track_names_of(events):
-    return sorted(set(t for t in events if _TRACK_RE.match(t)))
+    # the regex runs over the distinct tokens (a few hundred), not the song
+    return sorted(t for t in set(events) if _TRACK_RE.match(t))
 
 
 def bar_track_spans(events):
@@ -70,7 +71,17 @@ def mask_bar_and_track(event, vocab, mask_tracks, mask_bars):
     for a, b in reversed(pairs):
         del toks[a:a + max(0, b - a)]
         toks.insert(a, 'm_0')
-    return np.array([vocab.char2index(t) for t in toks]), mask_track_names, mask_bar_names
+    return _to_ids(vocab, toks), mask_track_names, mask_bar_names
+
+
+def _to_ids(vocab, toks):
+    """np.array([vocab.char2index(t) for t in toks]); one dict lookup per
+    token (char2index's per-call overhead dominated the host preparation)
+    unless some token is unknown (then char2index itself, for its report)."""
+    table = vocab._char2idx
+    if set(toks) - table.keys():
+        return np.array([vocab.char2index(t) for t in toks])
+    return np.fromiter((table[t] for t in toks), dtype=np.int64, count=len(toks))
 
 
 def decoder_targets(event, vocab, mask_tracks, mask_bars):
