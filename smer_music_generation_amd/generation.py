@@ -423,9 +423,13 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
             kv_reads = int(sum(len(q) * len(p[0]) + len(q) * (len(q) + 1) // 2
                                for q, p in zip(seqs, preps)))
             for sp, seq in zip(spans, seqs):
-                for idx in seq:
-                    _, chk, msg = sp.spec()
-                    sp.commit_greedy(idx, chk, msg)
+                if logger is None:  # no redraw report to log: commit only
+                    for idx in seq:
+                        sp.commit(idx)
+                else:
+                    for idx in seq:
+                        _, chk, msg = sp.spec()
+                        sp.commit_greedy(idx, chk, msg)
                 if not sp.done:
                     raise RuntimeError("device grammar and host replay disagree")
                 tokens += len(seq)
