@@ -169,6 +169,41 @@ __device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
   }
 }
 
+// LayerNorm of one row by one wave (lane c holds the 16-B chunks c, c+64, ..
+// of the row, N <= 2048): the statistics and the normalised value, shared by
+// ln_fwd_kernel and the decode Linear's LayerNorm prologue so that both
+// produce the same bits.
+constexpr int LNR_MAXC = 4;
+template <typename T>
+__device__ __forceinline__ void ln_row_stats(const T* __restrict__ xr, int N, float eps, int lane,
+                                             float (&v)[LNR_MAXC][8], float& mu, float& rs) {
+  const int nch = N >> 3;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < LNR_MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      load8<T>(xr + ch * 8, 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  mu = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < LNR_MAXC; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        q += d * d;
+      }
+  rs = rsqrtf(wave_sum(q) / N + eps);
+}
+__device__ __forceinline__ float ln_apply(float v, float mu, float rs, float g, float b) {
+  return __builtin_fmaf((v - mu) * rs, g, b);
+}
+
 // XCD-aware 2-D block index: blocks b and b+8 share an XCD (round-robin
 // dispatch), so give each XCD a contiguous run of the row-major work list;
 // x-neighbours (e.g. the query blocks of one (batch, head)) then share an L2.

@@ -45,35 +45,24 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
   const int nch = N >> 3;
-  float v[LN_MAXC][8];
-  float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, loaded with x
-  float s = 0.f;
+  float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, issued before x
 #pragma unroll
   for (int c = 0; c < LN_MAXC; ++c) {
-    int ch = lane + 64 * c;
+    const int ch = lane + 64 * c;
     if (ch < nch) {
-      Vec8<T>::load(x + (long)row * ldx + ch * 8, v[c]);
       Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
       Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s += v[c][i];
     }
   }
-  const float mu = wave_sum(s) / N;
-  float q = 0.f;
-#pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c)
-    if (lane + 64 * c < nch)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { float d = v[c][i] - mu; q += d * d; }
-  const float rs = rsqrtf(wave_sum(q) / N + eps);
+  float v[LNR_MAXC][8], mu, rs;
+  ln_row_stats<T>(x + (long)row * ldx, N, eps, lane, v, mu, rs);
 #pragma unroll
   for (int c = 0; c < LN_MAXC; ++c) {
     int ch = lane + 64 * c;
     if (ch < nch) {
       float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * rs * gb[c][i] + gb[c][8 + i];
+      for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gb[c][i], gb[c][8 + i]);
       Vec8<T>::store(y + (long)row * ldy + ch * 8, o);
     }
   }
