@@ -23,6 +23,7 @@ Decoder layers add the causal self-attention and the cross-attention
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -55,6 +56,7 @@ class Engine:
         self._fc_pad = None
         self._wgen = 0          # bumped whenever the working weights are rewritten
         self._ckv_all = None    # (key, W [L*2d, d], b [L*2d]) stacked cross-attn K/V projections
+        self._side = {}         # device -> (wgrad stream, its split-K workspace)
 
     # ------------------------------------------------------------------
     def act_dtype(self):
@@ -308,6 +310,38 @@ class Engine:
         return logits, wts, ctx
 
     # ------------------------------------------------------------------
+    def _wgrad_stream(self, dev, dt):
+        """Weight gradients run on a second HIP stream, overlapping the
+        dgrad / attention-backward chain on the main stream (they only feed
+        the optimizer).  bf16 only; SMER_WGRAD_OVERLAP=0 serialises."""
+        if dt != torch.bfloat16 or os.environ.get("SMER_WGRAD_OVERLAP", "1") == "0":
+            return None
+        side = self._side.get(dev)
+        if side is None:
+            side = (torch.cuda.Stream(device=dev),
+                    torch.empty(ops.SPLITK_WS_BYTES, dtype=torch.uint8, device=dev))
+            self._side[dev] = side
+        return side
+
+    @staticmethod
+    def _wgrad(side, dy, x, gw, **kw):
+        if side is None:
+            ops.linear_wgrad(dy, x, gw, **kw)
+            return
+        stream, ws = side
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            ops.linear_wgrad(dy, x, gw, ws=ws, **kw)
+        # temporaries freed on the main stream must not be reused before the
+        # side stream has read them
+        dy.record_stream(stream)
+        x.record_stream(stream)
+
+    @staticmethod
+    def _join(side):
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side[0])
+
     def backward(self, ctx, dlog_pad, hook=None):
         """dlog_pad: [B*T, Vp] activation dtype (cols >= V zero).  Accumulates
         every parameter gradient into the flat grad buffer.  `hook(name)` is
@@ -325,14 +359,17 @@ class Engine:
         Mt, Ms = B * T, B * S
 
         # vocab head
+        side = self._wgrad_stream(dev, dt)
+        wg = lambda *a, **kw: self._wgrad(side, *a, **kw)  # noqa: E731
+        wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
-        ops.linear_wgrad(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         # final decoder norm
         y_last, mo, ro = ctx.dec_last
         dy = torch.empty_like(y_last)
         ops.layernorm_bwd(g_out, y_last, mo, ro, W.dec_norm[0], dy, dgamma=G.dec_norm[0],
                           dbeta=G.dec_norm[1])
         if hook:
+            self._join(side)
             hook("head")
         # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
         # one dgrad GEMM (K = L*2d) after the decoder loop gives dmemory
@@ -346,40 +383,41 @@ class Engine:
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1])
+            wg(dy3d, h, GL.l2_w, db=GL.l2_b)
             dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
-            ops.linear_wgrad(dy3d, h, GL.l2_w, db=GL.l2_b)
+            wg(dh, x2, GL.l1_w, db=GL.l1_b)
             dx2 = ops.linear_dgrad(dh, L.l1_w, residual=dy3)
-            ops.linear_wgrad(dh, x2, GL.l1_w, db=GL.l1_b)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx2, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+            wg(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             doc = ops.linear_dgrad(dy2d, L.ca_ow)
-            ops.linear_wgrad(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)))
+            wg(dqc, x1, GL.cq_w, db=GL.cq_b)
+            wg(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
             dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
-            ops.linear_wgrad(dqc, x1, GL.cq_w, db=GL.cq_b)
-            ops.linear_wgrad(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
             # self-attention block
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+            wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             do = ops.linear_dgrad(dy1d, L.sa_ow)
-            ops.linear_wgrad(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
                          seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)))
+            wg(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             dy = ops.linear_dgrad(dqkv, L.sa_w, residual=dy1)
-            ops.linear_wgrad(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             if hook:
+                self._join(side)
                 hook("dec%d" % i)
         d_tgt = dy
         if self.n_dec:
@@ -398,28 +436,30 @@ class Engine:
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+            wg(dy2d, h, GL.l2_w, db=GL.l2_b)
             dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
-            ops.linear_wgrad(dy2d, h, GL.l2_w, db=GL.l2_b)
+            wg(dh, x1, GL.l1_w, db=GL.l1_b)
             dx1 = ops.linear_dgrad(dh, L.l1_w, residual=dy2)
-            ops.linear_wgrad(dh, x1, GL.l1_w, db=GL.l1_b)
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
                               drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+            wg(dy1d, o, GL.out_w, db=GL.out_b)
             do = ops.linear_dgrad(dy1d, L.out_w)
-            ops.linear_wgrad(dy1d, o, GL.out_w, db=GL.out_b)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
                          seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)))
+            wg(dqkv, x_in, GL.in_w, db=GL.in_b)
             dx = ops.linear_dgrad(dqkv, L.in_w, residual=dy1)
-            ops.linear_wgrad(dqkv, x_in, GL.in_w, db=GL.in_b)
             if hook:
+                self._join(side)
                 hook("enc%d" % i)
         # shared embedding (model.py:76): both streams scatter into one table
         ops.embed_bwd(G.emb, math.sqrt(d), [(ctx.src_ids, dx, ctx.p_pos, sd(_SITE["pe_src"])),
                                             (ctx.tgt_ids, d_tgt, ctx.p_pos, sd(_SITE["pe_tgt"]))])
+        self._join(side)
         if hook:
             hook("embedding")
 

@@ -153,13 +153,16 @@ def linear_dgrad(dy, w, *, K=None, out=None, residual=None, gate=None, gate_scal
     return out if out is not None else out_f32
 
 
-def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None):
+def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None, ws=None):
     """dw (+)= dy^T @ x: dy [T, M_out(ld)], x [T, K_in] -> dw fp32 [M_out, K_in];
-    db (+)= column sums of dy when given (bf16: fused into the GEMM)."""
+    db (+)= column sums of dy when given (bf16: fused into the GEMM).  `ws`:
+    split-K slab buffer (default: the per-device one; a second stream running
+    wgrads concurrently passes its own)."""
     T = dy.shape[0]
     Mo = M if M is not None else dy.shape[1]
     if db is not None and dy.dtype == torch.bfloat16:
-        ws = splitk_workspace(dy.device)
+        if ws is None:
+            ws = splitk_workspace(dy.device)
         timer = GEMM_TIMER
         if timer is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
