@@ -9,6 +9,9 @@ R=$PWD
 TAG=${1:-r01}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
+# per-kernel durations in isolation: weight gradients on the main stream,
+# as in bench.py's event-timed steps (the product path overlaps them)
+export SMER_WGRAD_OVERLAP=0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $R/bench.py --steps 5 --warmup 2 --no-infill --no-cpu --no-c4 > $OUT/trace.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
@@ -17,4 +20,7 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write
   python3 $R/bench.py --steps 2 --warmup 1 --no-infill --no-cpu --no-roofline --no-c4 > $OUT/write.log 2>&1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dec -o run -- \
   python3 $R/tools/prof_decode.py --n 50 --graph > $OUT/dec.log 2>&1
+# the product path (weight-gradient stream overlap on), timed steps only
+SMER_WGRAD_OVERLAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_ovl -o run -- \
+  python3 $R/bench.py --steps 5 --warmup 2 --no-infill --no-cpu --no-c4 --no-roofline > $OUT/trace_ovl.log 2>&1
 echo done

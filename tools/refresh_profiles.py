@@ -30,10 +30,20 @@ train = run(os.path.join(ROOT, "tools", "prof_summary.py"),
             os.path.join(src, "trace", "run_kernel_stats.csv"), steps, "30")
 with open(os.path.join(dst, tag + "_train_kernel_stats.txt"), "w") as f:
     f.write("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 "
-            "--no-infill --no-cpu --no-c4  (%s steps traced: 2 warm-up + 5 timed + 5 "
+            "--no-infill --no-cpu --no-c4  with SMER_WGRAD_OVERLAP=0, i.e. weight gradients on the "
+            "main stream so each kernel's duration is its own (%s steps traced: 2 warm-up + 5 timed + 5 "
             "event-timed; per-step = total/%s)\n" % (steps, steps) + train)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
             os.path.join(dst, tag + "_train_kernel_stats.csv"))
+
+ovl = os.path.join(src, "trace_ovl", "run_kernel_stats.csv")
+if os.path.exists(ovl):
+    t = run(os.path.join(ROOT, "tools", "prof_summary.py"), ovl, "7", "30")
+    with open(os.path.join(dst, tag + "_train_overlap_kernel_stats.txt"), "w") as f:
+        f.write("# rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 --warmup 2 "
+                "--no-infill --no-cpu --no-c4 --no-roofline  (product path: weight gradients on "
+                "a second stream, concurrent with the main chain, so kernel durations overlap; "
+                "7 steps traced; per-step = total/7)\n" + t)
 
 dec = run(os.path.join(ROOT, "tools", "prof_summary.py"),
           os.path.join(src, "dec", "run_kernel_stats.csv"), "51", "20")
