@@ -90,9 +90,11 @@ def bench_train(args, dev, rank, world):
         prev = os.environ.get("SMER_WGRAD_OVERLAP")
         os.environ["SMER_WGRAD_OVERLAP"] = "0"
         try:
+            ts0 = time.perf_counter()
             for _ in range(args.steps):
                 tr.step(bt)
             torch.cuda.synchronize()
+            t_serial = time.perf_counter() - ts0
         finally:
             ops.GEMM_TIMER = None
             if prev is None:
@@ -116,7 +118,9 @@ def bench_train(args, dev, rank, world):
         achieved = s["flops"] / (s["total_ms"] / 1e3) / 1e12
         res["gemm"] = {"launches": s["launches"], "avg_us": 1000 * s["total_ms"] / max(1, s["launches"]),
                        "flops_per_launch": s["flops"] / max(1, s["launches"]),
-                       "tflops": achieved, "share_of_step": s["total_ms"] / (1000 * dt),
+                       "tflops": achieved,
+                       # GEMM time over the wall time of the SAME (serialised) steps
+                       "share_of_step": s["total_ms"] / (1000 * t_serial),
                        "timed_over": "%d extra steps after the timed ones, weight gradients "
                                      "on the main stream (no concurrent kernels)" % args.steps}
     return res
@@ -135,17 +139,24 @@ def bench_train_c4(args, dev, rank, world):
 
 
 def _infill_requests(n, target_len=1024, seed0=0, n_infill_bars=2):
-    """n synthetic 3-track songs of ~target_len SMER tokens, each request
-    infilling one track over its last-but-two n_infill_bars bars."""
+    """n synthetic 3-track songs whose MASKED source (the encoder input) holds
+    at least target_len SMER tokens, each request infilling one track over
+    its last-but-two n_infill_bars bars."""
+    from smer_music_generation_amd.generation import _prepare
     from smer_music_generation_amd.synth import synth_events
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, CTRL)
     reqs = []
     for i in range(n):
-        nb = 8
-        ev = synth_events(seed0 + i, n_bars=nb, n_tracks=3)
-        while len(ev) < target_len - 120:
-            nb += 2 if target_len <= 1024 else 8
+        nb = max(8, target_len // 80)
+        while True:
             ev = synth_events(seed0 + i, n_bars=nb, n_tracks=3)
-        bars = list(range(nb - 2 - n_infill_bars, nb - 2))
+            bars = list(range(nb - 2 - n_infill_bars, nb - 2))
+            n_src = len(_prepare(list(ev), v, [i % 3], bars)[0])
+            if n_src >= target_len:
+                break
+            # jump close to the target, then step bar by bar
+            nb = max(nb + 1, int(nb * target_len / n_src) - 1)
         reqs.append((ev, [i % 3], bars))
     return reqs
 
@@ -190,6 +201,35 @@ def bench_infill(args, dev, rank):
             "roofline": infill_roofline(args, st)}
 
 
+def bench_infill_batch1(args, dev, rank):
+    """The plugin call itself: one `generation_all` (reference signature and
+    defaults: weighted sampling, batch 1, host grammar loop per token over the
+    KV-cached session) on a C2-model request with an S>=1024 source."""
+    from smer_music_generation_amd.generation import generation_all
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, CTRL)
+    m = make_model(args, dev).eval()
+    ac = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
+    (wev, wtr, wbr), = _infill_requests(1, args.seq, 8100 + rank)
+    np.random.seed(1)
+    generation_all(m, list(wev), dev, v, None, ac, wtr, wbr)  # warm-up (graph capture)
+    reqs = _infill_requests(8, args.seq, 8000 + 100 * rank)
+    from smer_music_generation_amd.generation import _prepare
+    src_len = float(np.mean([len(_prepare(list(ev), v, tr, br)[0]) for ev, tr, br in reqs]))
+    np.random.seed(0)
+    steps = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for ev, tr, br in reqs:  # one plugin call per request, back to back
+        stats = {}
+        if generation_all(m, list(ev), dev, v, None, ac, tr, br, stats=stats) is not None:
+            steps += stats["steps"]
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 1), "tokens": steps, "seconds": round(dt, 4),
+            "requests": len(reqs), "mean_src_len": round(src_len, 1),
+            "ms_per_token": round(1000 * dt / max(1, steps), 3)}
+
+
 def bench_infill_c5(args, dev, rank):
     """BASELINE.json configs[4]: 64 concurrent requests,
     sources of ~4096 SMER tokens, each infilling 4 bars of one track, greedy,
@@ -220,14 +260,32 @@ def bench_infill_c5(args, dev, rank):
             "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s")}}
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """The oracle (torch-CPU fp32 restatement of the reference step) on a
-    bounded sample of the same workload: B=2 sequences of the C2 shape."""
+    """The oracle (torch-CPU fp32 restatement of the reference path) on the
+    GPU box's host, on bounded samples of the same workloads:
+      train  — B=2 sequences of the C2 step shape (fwd + bwd);
+      infill — the reference's decode algorithm (full recompute of encoder +
+               decoder per token, generation.py:209-225,542-545) on one C2
+               request with an S>=1024 source, greedy, ~10 s of tokens.
+    Threads: torch.set_num_threads(os.cpu_count()) as BASELINE.md asks,
+    unless the box pins this job's CPU share in OMP_NUM_THREADS (the GPU box
+    does: 16), which is then used and reported."""
     from oracle import ref_cpu
+    from smer_music_generation_amd.generation import _prepare
     from smer_music_generation_amd.synth import synth_training_batch
     from smer_music_generation_amd.vocab import WordVocab
-    threads = os.cpu_count() or 1
-    threads = min(threads, 16)
+    ncpu = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or ncpu
     torch.set_num_threads(threads)
     v = WordVocab(0, CTRL)
     cfg = dict(d_model=args.d_model, nhead=args.nhead, num_encoder_layers=args.layers,
@@ -245,10 +303,40 @@ def cpu_baseline(args):
         if time.perf_counter() - t0 > 10.0 or n >= 5:
             break
     dt = time.perf_counter() - t0
-    return {"value": B * (args.seq + args.tgt) * n / dt, "unit": "tokens/s", "cores": threads,
-            "kind": "port",
-            "sample": "%d oracle train steps (fwd+bwd, fp32, torch CPU) at B=%d S=%d T=%d, C2 model"
-                      % (n, B, args.seq, args.tgt)}
+    res = {"value": B * (args.seq + args.tgt) * n / dt, "unit": "train tokens/s (B*(S+T))",
+           "cores": threads, "os_cpu_count": ncpu, "cpu_model": _cpu_model(), "kind": "port",
+           "sample": "%d oracle train steps (fwd+bwd, fp32, torch CPU) at B=%d S=%d T=%d, C2 model"
+                     % (n, B, args.seq, args.tgt)}
+    # infill: the reference algorithm, full recompute per token
+    ev, tracks, bars = _infill_requests(1, args.seq, 4242)[0]
+    src, _, _, target, no_whole = _prepare(list(ev), v, tracks, bars)
+    fn = ref_cpu.full_recompute_logits_fn(sd, cfg)
+    calls = [0]
+    t_end = [None]
+
+    class _Budget(Exception):
+        pass
+
+    def timed(src_ids, tgt_list):
+        if time.perf_counter() > t_end[0]:
+            raise _Budget()
+        calls[0] += 1
+        return fn(src_ids, tgt_list)
+    ac = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
+    fn(src, [2])  # warm-up
+    t0 = time.perf_counter()
+    t_end[0] = t0 + 10.0
+    try:
+        ref_cpu.infill(timed, src, target, v, ac, no_whole, greedy=True)
+    except _Budget:
+        pass
+    dt = time.perf_counter() - t0
+    res["infill"] = {"value": calls[0] / dt, "unit": "infill tokens/s (batch 1)", "cores": threads,
+                     "kind": "port",
+                     "sample": "%d greedy decode tokens of one C2 request (S=%d), full recompute "
+                               "per token as generation.py:209-225 (oracle fp32 torch CPU)"
+                               % (calls[0], len(src))}
+    return res
 
 
 def _pmc_traffic():
@@ -327,6 +415,7 @@ def main():
             sec = t[1:2].clone()
             dist.all_reduce(sec, op=dist.ReduceOp.MAX)
             inf["tokens_per_s"] = tok.item() / sec.item()
+    b1 = bench_infill_batch1(args, dev, rank) if args.infill else None
     c5 = None
     if args.infill and args.c5:
         c5 = bench_infill_c5(args, dev, rank)
@@ -373,7 +462,10 @@ def main():
                                "decode_steps": inf["steps"], "tokens": inf["tokens"],
                                "ms_per_decode_step": round(inf["ms_per_decode_step"], 3),
                                "roofline": inf["roofline"],
-                               "phases_s": inf["phases_s"], "parallelism": "replicas"},
+                               "phases_s": inf["phases_s"], "parallelism": "replicas",
+                               "batch1": b1 and dict(b1, metric="plugin call generation_all "
+                                                     "(batch 1, default weighted sampling, "
+                                                     "KV-cached), tokens/s")},
             "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
                                           "S=2048 T=512, bf16",
                                 "value": round(c4["tokens_per_s"], 1),

@@ -329,7 +329,7 @@ class Engine:
             ops.linear_wgrad(dy, x, gw, **kw)
             return
         stream, ws = side
-        stream.wait_stream(torch.cuda.current_stream())
+        stream.wait_stream(torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(stream):
             ops.linear_wgrad(dy, x, gw, ws=ws, **kw)
         # temporaries freed on the main stream must not be reused before the
@@ -340,7 +340,7 @@ class Engine:
     @staticmethod
     def _join(side):
         if side is not None:
-            torch.cuda.current_stream().wait_stream(side[0])
+            torch.cuda.current_stream(side[0].device).wait_stream(side[0])
 
     def backward(self, ctx, dlog_pad, hook=None):
         """dlog_pad: [B*T, Vp] activation dtype (cols >= V zero).  Accumulates

@@ -339,10 +339,11 @@ def _prepare(events, vocab, tracks_to_generate, bars_to_generate):
 
 
 def generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
-                   bars_to_generate, *, greedy=False, use_kv_cache=True):
+                   bars_to_generate, *, greedy=False, use_kv_cache=True, stats=None):
     """`generation.py:468-696`.  Returns (restored '<U9' tokens,
     mask_track_names, mask_bar_names) or None (nothing masked / on error,
-    after printing it, as the reference does)."""
+    after printing it, as the reference does).  `stats` (a dict, opt-in)
+    receives the number of decode steps (= tokens drawn)."""
     try:
         src, mtn, mbn, target, no_whole = _prepare(events, vocab, tracks_to_generate,
                                                    bars_to_generate)
@@ -351,6 +352,7 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
             return None
         model.eval()
         with torch.no_grad():
+            steps = 0
             if use_kv_cache:
                 sess = DecodeSession(model, 1, len(src), max(128, 100 * st.n_masks + 8))
                 sess.prefill([0], [src])
@@ -360,11 +362,15 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
                     logit = sess.step([(0, pre[fed:], fed)])[0]
                     fed = len(pre)
                     st.advance(logit)
+                    steps += 1
             else:
                 src_t = torch.tensor(src)
                 while not st.done:
                     out = model_generate(model, src_t, st.prefix(), device)
                     st.advance(out[-1].numpy())
+                    steps += 1
+            if stats is not None:
+                stats["steps"] = steps
         src_token = [vocab.index2char(int(t)) for t in src]
         return restore_marked_input(src_token, st.total), mtn, mbn
     except Exception as e:  # reference behaviour (generation.py:695-696)
@@ -469,5 +475,6 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         t3 = time.perf_counter()
         return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,
                      "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev,
-                     "request_latency_s": latency, "kv_row_reads": kv_reads}
+                     "request_latency_s": latency, "kv_row_reads": kv_reads,
+                     "generated": [list(st.total) for st in spans]}
     return out

@@ -291,6 +291,35 @@ class ScoreTransformer(nn.Module):
             self._engine = _engine.Engine(self)
         return self._engine
 
+    def _check_causal(self, tgt_mask, T):
+        """The engine's decoder self-attention is causal by construction, the
+        only mask the reference ever passes (`train.py:715`,
+        `generation.py:214`; only tgt_mask[0] is used, `model.py:95`).  Any
+        other mask (or none, which the reference would treat as
+        unmasked) raises instead of silently computing something else.
+        Checked once per mask tensor (keyed by storage and version)."""
+        if tgt_mask is None:
+            raise RuntimeError("tgt_mask=None (unmasked decoder self-attention) is not supported: "
+                               "pass the causal nopeek mask (gen_nopeek_mask)")
+        m = tgt_mask[0] if tgt_mask.dim() == 3 else tgt_mask
+        if tuple(m.shape) != (T, T):
+            raise RuntimeError("tgt_mask must be [T, T] or [B, T, T] with T=%d, got %s"
+                               % (T, tuple(tgt_mask.shape)))
+        key = (m.data_ptr(), m._version, T, str(m.device), m.dtype)
+        if getattr(self, "_causal_ok", None) == key:
+            return
+        upper = torch.ones(T, T, dtype=torch.bool, device=m.device).triu(1)
+        if m.dtype == torch.bool:
+            ok = torch.equal(m, upper)
+        else:
+            mf = m.float()
+            ok = bool(torch.all(torch.isneginf(mf[upper])).item()) and \
+                bool(torch.all(mf[~upper] == 0).item())
+        if not ok:
+            raise RuntimeError("tgt_mask is not the causal nopeek mask: the engine only computes "
+                               "causal decoder self-attention (the reference's only mask)")
+        self._causal_ok = key
+
     # ---- reference forward ---------------------------------------------
     def forward(self, src, tgt, src_key_padding_mask, tgt_key_padding_mask,
                 memory_key_padding_mask, tgt_mask):
@@ -299,6 +328,7 @@ class ScoreTransformer(nn.Module):
         mask (`train.py:1356-1369`); only tgt_mask[0] is used (`model.py:95`)."""
         if src.size(0) != tgt.size(0):
             raise RuntimeError("the batch number of src and tgt must be equal")
+        self._check_causal(tgt_mask, tgt.size(1))
         need_grad = torch.is_grad_enabled() and self.embedding.weight.requires_grad
         return _engine.ScoreTransformerFunction.apply(
             self.embedding.weight, self, need_grad, src, tgt, src_key_padding_mask, tgt_key_padding_mask,

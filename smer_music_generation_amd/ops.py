@@ -189,10 +189,32 @@ def attn_drop_mask(B, H, Lq, Lk, device):
     return torch.empty(max(16, n), dtype=torch.uint8, device=device)
 
 
+_WARNED_P = set()
+
+
+def attn_drop_rate(p):
+    """Realised attention-probability dropout rate: the attention kernels
+    draw keep decisions at 1/128 granularity (csrc/common.h smer_attn_thr7:
+    round(128 p) clamped to [1, 127]), survivors scaled exactly for it."""
+    if p <= 0:
+        return 0.0
+    return min(127, max(1, int(p * 128.0 + 0.5))) / 128.0
+
+
+def _check_attn_p(p):
+    r = attn_drop_rate(p)
+    if p > 0 and abs(r - p) > 0.1 * p and p not in _WARNED_P:
+        import warnings
+        _WARNED_P.add(p)
+        warnings.warn("attention dropout p=%g is realised as %g (1/128 granularity of the "
+                      "attention kernels); activation dropout sites keep p to 1/65536" % (p, r))
+
+
 def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale, drop_p=0.0,
              seed=0, drop_mask=None, drop_mask_in=False):
     """drop_mask: keep-bit buffer the forward fills (hashing) for the
     backward, or, with drop_mask_in, reads (from attn_drop_mask_gen)."""
+    _check_attn_p(drop_p)
     call("smer_attn_fwd", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k),
          _p(v), _ld(v), _p(o), _ld(o), _p(lse), _p(kpm), int(causal), float(scale),
          float(drop_p), int(seed) & 0xFFFFFFFF, _p(drop_mask), int(bool(drop_mask_in)), _stream())
