@@ -88,6 +88,14 @@ class Engine:
         self._fc_pad = None
         self._wgen += 1
 
+    def mark_params_updated(self):
+        """The fp32 master was rewritten through a raw pointer (fused Adam):
+        torch's version counters did not move, so invalidate every cached
+        derivative of the weights (bf16 copy, stacked cross-attention K/V)."""
+        self._bf16_version = None
+        self._fc_pad = None
+        self._wgen += 1
+
     def weights(self, dt):
         """Per-layer views of the working weights (bf16 copy or fp32 master);
         biases / norms always fp32 master."""

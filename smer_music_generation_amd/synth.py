@@ -47,8 +47,11 @@ def _bar_notes(rng, sixteenths, allow_whole):
     return out
 
 
-def synth_events(seed, n_bars=4, n_tracks=2, time_signature="4/4"):
-    """A plugin-format SMER event list (strings)."""
+def synth_events(seed, n_bars=4, n_tracks=2, time_signature="4/4", copy_controls=True):
+    """A plugin-format SMER event list (strings).  copy_controls=False gives
+    the encoder's layout before `change_controls` (generation.py:698-877)
+    copies each track's controls to the track end and the bar's tensile to
+    the bar end."""
     rng = np.random.default_rng(seed)
     num, den = int(time_signature[0]), int(time_signature[2])
     sixteenths = num * (4 if den == 4 else 2)
@@ -64,8 +67,11 @@ def synth_events(seed, n_bars=4, n_tracks=2, time_signature="4/4"):
         for t in range(n_tracks):
             ctl = ["d_%d" % int(rng.integers(10)), "o_%d" % int(rng.integers(10)),
                    "y_%d" % int(rng.integers(10))]
-            ev += ["track_%d" % t] + ctl + _bar_notes(rng, sixteenths, allow_whole) + ctl
-        ev.append(tens)
+            ev += ["track_%d" % t] + ctl + _bar_notes(rng, sixteenths, allow_whole)
+            if copy_controls:
+                ev += ctl
+        if copy_controls:
+            ev.append(tens)
     return ev
 
 

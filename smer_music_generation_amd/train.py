@@ -113,6 +113,83 @@ def layer_ranges(model):
     return r
 
 
+class FusedAdam(torch.optim.Optimizer):
+    """`torch.optim.Adam`'s state and param_groups over the Trainer's flat
+    moment buffers (train.py:264 builds `Adam(model.parameters(), lr)`).
+
+    The update itself is the Trainer's fused kernel; this object exists so
+    that the reference's surrounding code works unchanged:
+      * `state_dict()` / `load_state_dict()` in torch Adam's format, so a
+        reference checkpoint's `optimizer_state_dict` (train.py:266-303,
+        970-971) resumes here and ours resumes in torch Adam;
+      * `param_groups[0]['lr']` is read every step, so
+        `ReduceLROnPlateau(trainer.optimizer, ...)` (train.py:663-664, 939)
+        drives the fused step.
+    Per-parameter `exp_avg` / `exp_avg_sq` are views of the flat buffers."""
+
+    def __init__(self, model, m, v, lr, betas, eps):
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=0, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False,
+                        fused=None, decoupled_weight_decay=False)
+        super().__init__(list(model.parameters()), defaults)
+        self._m, self._v = m, v
+        self._views = []
+        for name, p in model.named_parameters():
+            o = model._offsets[name]
+            n = p.numel()
+            self._views.append((p, m[o: o + n].view(p.shape), v[o: o + n].view(p.shape)))
+        self.t = 0
+
+    def step(self, closure=None):
+        raise RuntimeError("FusedAdam is stepped by Trainer.step (fused kernel)")
+
+    def zero_grad(self, set_to_none=False):
+        for p, _, _ in self._views:
+            if p.grad is not None:
+                p.grad.zero_()
+
+    def state_dict(self):
+        state = {}
+        if self.t > 0:
+            for i, (_, ma, va) in enumerate(self._views):
+                state[i] = {"step": torch.tensor(float(self.t)), "exp_avg": ma.detach().clone(),
+                            "exp_avg_sq": va.detach().clone()}
+        groups = []
+        for g in self.param_groups:
+            d = {k: v for k, v in g.items() if k != "params"}
+            d["params"] = list(range(len(self._views)))
+            groups.append(d)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, state_dict):
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self._views):
+            raise ValueError("optimizer state has %d groups / %s params, expected 1 / %d"
+                             % (len(groups), [len(g["params"]) for g in groups], len(self._views)))
+        for k in ("lr", "betas", "eps", "weight_decay", "amsgrad"):
+            if k in groups[0]:
+                self.param_groups[0][k] = groups[0][k]
+        if self.param_groups[0].get("weight_decay", 0) or self.param_groups[0].get("amsgrad"):
+            raise ValueError("FusedAdam implements Adam without weight decay / amsgrad (train.py:264)")
+        st = state_dict["state"]
+        steps = set()
+        order = groups[0]["params"]
+        for slot, pid in enumerate(order):
+            s = st.get(pid)
+            _, ma, va = self._views[slot]
+            if s is None:
+                ma.zero_()
+                va.zero_()
+                steps.add(0)
+                continue
+            ma.copy_(s["exp_avg"].reshape(ma.shape).to(ma.device, ma.dtype))
+            va.copy_(s["exp_avg_sq"].reshape(va.shape).to(va.device, va.dtype))
+            steps.add(int(float(s["step"])))
+        if len(steps) > 1:
+            raise ValueError("per-parameter Adam steps differ %s; the fused step shares one" % steps)
+        self.t = steps.pop() if steps else 0
+
+
 class Trainer:
     """One optimizer step per `step(batch)`; DP across the default process
     group when torch.distributed is initialised (world_size > 1)."""
@@ -121,7 +198,6 @@ class Trainer:
                  group=None):
         self.model = model
         self.vocab = vocab
-        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
         dev = model.flat_parameters().device
         w, ce_all = criterion_vectors(vocab, eos_weight, dev)
         self.crit_w = w
@@ -130,11 +206,36 @@ class Trainer:
         n = model.flat_parameters().numel()
         self.m = torch.zeros(n, device=dev)
         self.v = torch.zeros(n, device=dev)
-        self.t = 0
+        self.optimizer = FusedAdam(model, self.m, self.v, lr, betas, eps)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self._ranges = layer_ranges(model)
         self._seed = 1
+
+    # hyper-parameters live in the optimizer's param group (schedulers edit it)
+    @property
+    def lr(self):
+        return self.optimizer.param_groups[0]["lr"]
+
+    @lr.setter
+    def lr(self, value):
+        self.optimizer.param_groups[0]["lr"] = float(value)
+
+    @property
+    def t(self):
+        return self.optimizer.t
+
+    @t.setter
+    def t(self, value):
+        self.optimizer.t = int(value)
+
+    def state_dict(self):
+        """torch Adam format (`optimizer_state_dict` of train.py:970-971)."""
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, state_dict):
+        self.optimizer.load_state_dict(state_dict)
+        self.model.engine.mark_params_updated()  # weights may have been reloaded too
 
     def set_eos_weight(self, eos_weight):
         """Pretrain -> finetune switch (train.py:670-676)."""
@@ -180,12 +281,13 @@ class Trainer:
             bucketer.finish()
         self.t += 1
         work = eng._bf16 if eng.act_dtype() == torch.bfloat16 and eng._bf16 is not None else None
-        ops.adam(model.flat_parameters(), grad, self.m, self.v, work, lr=self.lr, b1=self.b1,
-                 b2=self.b2, eps=self.eps, step=self.t)
+        g = self.optimizer.param_groups[0]
+        ops.adam(model.flat_parameters(), grad, self.m, self.v, work, lr=g["lr"], b1=g["betas"][0],
+                 b2=g["betas"][1], eps=g["eps"], step=self.t)
         if work is not None:
             eng.mark_bf16_fresh()
         else:
-            eng._bf16_version = None
+            eng.mark_params_updated()
         if return_parts:
             return loss, self.loss_parts(row_loss, y, denom)
         return loss

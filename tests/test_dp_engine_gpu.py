@@ -1,0 +1,174 @@
+"""The engine's data-parallel path on the GPU.
+
+* The weight-gradient side stream (bf16) changes nothing: flat gradients with
+  SMER_WGRAD_OVERLAP=1 equal the serialised run bit for bit, and every
+  layer range is already final when its backward hook fires (the hook is
+  where GradBucketer issues that range's all-reduce).
+* Trainer.step all-reduces the loss normaliser BEFORE the fused CE
+  (train.py:736-742 normalises over the whole batch), then sums gradients.
+* Two ranks over gloo on one GPU, each with half the batch, through the real
+  Trainer.step / Engine.backward hooks / GradBucketer, equal the
+  single-process step on the concatenated batch.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests.dp_engine_common import build, make_batch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _mid_model_and_ctx(seed=0):
+    from smer_music_generation_amd.model import ScoreTransformer
+    from smer_music_generation_amd.synth import synth_training_batch
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, ['key', 'tensile', 'density', 'polyphony', 'occupation'])
+    torch.manual_seed(seed)
+    m = ScoreTransformer(309, 512, 8, 2, 2, 2048, 2400, 0.1, 0.1).to("cuda")
+    b = synth_training_batch(77, v, 2, 1024, 256)
+    return m, {k: torch.from_numpy(np.asarray(x)).to("cuda") for k, x in b.items()}
+
+
+def _fwd_bwd(m, bt, hook=None):
+    from smer_music_generation_amd import ops
+    from smer_music_generation_amd.train import criterion_vectors
+    from smer_music_generation_amd.vocab import WordVocab
+    eng = m.engine
+    v = WordVocab(0, ['key', 'tensile', 'density', 'polyphony', 'occupation'])
+    logits, _, ctx = eng.forward(bt["input"], bt["target_in"], bt["input_pad_mask"],
+                                 bt["target_pad_mask"], bt["input_pad_mask"], training=True,
+                                 need_weights=False, save=True, seed=12345)
+    w, ce_all = criterion_vectors(v, 0.8, "cuda")
+    y = bt["target_out"].reshape(-1).long()
+    denom = torch.empty(1, device="cuda")
+    ops.wce_denom(y, ce_all, denom)
+    dlog = torch.zeros(y.numel(), eng.Vp, dtype=ctx.dt, device="cuda")
+    row = torch.empty(y.numel(), device="cuda")
+    ops.wce_fwd_bwd(logits, y, sum(w.values()), denom, row, None, dlog, V=eng.V)
+    g = m.flat_grad()
+    g.zero_()
+    eng.backward(ctx, dlog, hook=hook)
+    torch.cuda.synchronize()
+    return g.clone()
+
+
+def test_bf16_wgrad_stream_bitexact_and_ranges_final_at_hook(monkeypatch):
+    """d512 / S1024 bf16 with dropout; overlap on == off bit for
+    bit (deterministic split-K), and each hook sees its range final."""
+    from smer_music_generation_amd.train import layer_ranges
+    m, bt = _mid_model_and_ctx()
+    monkeypatch.setenv("SMER_WGRAD_OVERLAP", "0")
+    g0 = _fwd_bwd(m, bt)
+    monkeypatch.setenv("SMER_WGRAD_OVERLAP", "1")
+    ranges = layer_ranges(m)
+    seen = {}
+
+    def hook(name):
+        a, b = ranges[name]
+        seen[name] = m.flat_grad()[a:b].clone()   # on the main stream, at hook time
+    g1 = _fwd_bwd(m, bt, hook)
+    assert torch.equal(g0, g1)
+    assert set(seen) == set(ranges)
+    for name, snap in seen.items():
+        a, b = ranges[name]
+        assert torch.equal(snap, g1[a:b]), name
+
+
+class _FakeWork:
+    def wait(self):
+        pass
+
+
+class _FakeDist:
+    """Two identical ranks: every all-reduce doubles its tensor in place."""
+
+    def __init__(self, log):
+        self.log = log
+        self.ReduceOp = torch.distributed.ReduceOp
+
+    def all_reduce(self, t, op=None, group=None, async_op=False):
+        self.log.append(("all_reduce", t.numel()))
+        t.mul_(2.0)
+        return _FakeWork() if async_op else None
+
+    def is_available(self):
+        return True
+
+    def is_initialized(self):
+        return True
+
+    def get_world_size(self, group=None):
+        return 2
+
+
+def test_trainer_reduces_denominator_before_fused_ce(monkeypatch):
+    from smer_music_generation_amd import ops
+    from smer_music_generation_amd import train as T
+    m, v = build("cuda")
+    b = make_batch(v)
+    bt = {k: torch.from_numpy(np.asarray(x)).to("cuda") for k, x in b.items()}
+    ref = T.Trainer(m, v)
+    loss1 = ref.step(bt)
+    g1 = m.flat_grad().clone()
+    m2, _ = build("cuda")
+    log = []
+    monkeypatch.setattr(T, "dist", _FakeDist(log))
+    orig = ops.wce_fwd_bwd
+
+    def wce(*a, **kw):
+        log.append(("wce", 0))
+        return orig(*a, **kw)
+    monkeypatch.setattr(T.ops, "wce_fwd_bwd", wce)
+    tr = T.Trainer(m2, v)
+    assert tr.world == 2
+    loss2 = tr.step(bt)
+    torch.cuda.synchronize()
+    assert log[0] == ("all_reduce", 1) and log[1] == ("wce", 0), log[:3]
+    # every other all-reduce is a gradient range, one per layer hook
+    assert len(log) - 2 == len(T.layer_ranges(m2))
+    # identical "ranks": global denominator 2d, summed gradients 2 * g/(2d)
+    assert torch.equal(m2.flat_grad(), g1)
+    assert abs(2 * loss2.item() - loss1.item()) < 1e-6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_gloo_engine_matches_single_process(tmp_path):
+    from smer_music_generation_amd.train import Trainer
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path)]
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    m, v = build("cuda")
+    b = make_batch(v)
+    bt = {k: torch.from_numpy(np.asarray(x)).to("cuda") for k, x in b.items()}
+    loss = Trainer(m, v).step(bt)
+    g = m.flat_grad().cpu()
+    for rk in range(2):
+        got = torch.load(os.path.join(tmp_path, "rank%d.pt" % rk), weights_only=True)
+        assert abs(float(got["loss"]) - loss.item()) < 1e-5 * max(1.0, loss.item())
+        err = float((got["grad"] - g).norm() / g.norm())
+        assert err < 1e-5, (rk, err)

@@ -299,3 +299,45 @@ def test_device_grammar_matches_host_loop(golden_dir, precision):
     if precision == "fp32":
         for rec, got in zip([r for r in g["cases"] if r["mode"] == "greedy"], a):
             assert [str(x) for x in got[0]] == rec["restored"]
+
+
+@pytest.mark.parametrize("precision,ltol,ptol", [("fp32", 1e-4, 1e-5), ("bf16", 3e-2, 2e-3)])
+def test_three_fused_steps_track_oracle(precision, ltol, ptol):
+    """Three Trainer steps (fused CE + backward + fused Adam) vs three oracle
+    steps (reference autograd + torch Adam): the weights the 2nd / 3rd
+    forward sees must be the updated ones (every cached derivative of the
+    weights — bf16 copy, stacked cross-attention K/V — refreshed after the
+    raw-pointer Adam update).  eps = 1 and lr = 0.5 keep Adam's update
+    linear in the gradient (at eps = 1e-8 the first steps are lr * sign(g),
+    which amplifies round-off on near-zero gradients) and large enough that
+    stale weights would show in the next loss."""
+    from oracle import ref_cpu
+    from smer_music_generation_amd.model import ScoreTransformer
+    from smer_music_generation_amd.train import Trainer
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, CTRL)
+    torch.manual_seed(6)
+    m = ScoreTransformer(309, 128, 4, 2, 2, 256, 2400, 0.0, 0.0, precision=precision)
+    sd = {k: t.detach().clone() for k, t in m.state_dict().items()}
+    m = m.to(dev)
+    b = _oracle_batch(v, 2, 96, 24, 13)
+    cfg = dict(d_model=128, nhead=4, num_encoder_layers=2, num_decoder_layers=2)
+    lr, eps = 0.5, 1.0
+    tr = Trainer(m, v, lr=lr, eps=eps)
+    bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
+    params = {k: t for k, t in sd.items() if k != "pos_enc.pe"}
+    mo = {k: torch.zeros_like(t) for k, t in params.items()}
+    vo = {k: torch.zeros_like(t) for k, t in params.items()}
+    losses = []
+    for step in range(1, 4):
+        rl, _, grads, _ = ref_cpu.train_step(sd, cfg, b, v.control_indices, 0.8, 8)
+        loss = tr.step(bt)
+        losses.append((loss.item(), float(rl)))
+        ref_cpu.adam_step(params, grads, mo, vo, step, lr=lr, eps=eps)
+        sd.update(params)
+    for got, ref in losses:
+        assert abs(got - ref) < ltol * max(1, ref), losses
+    assert losses[2][1] < losses[0][1] - 1e-3, losses  # the steps move the loss
+    for name, p in m.named_parameters():
+        err = fro_rel(p.detach().cpu().numpy(), params[name].numpy())
+        assert err < ptol, (name, err)
