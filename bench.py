@@ -33,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 CTRL = ['key', 'tensile', 'density', 'polyphony', 'occupation']
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+FP8_PEAK_TFLOPS = 5000.0    # MI355X dense fp8 MFMA (block-scaled e4m3)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec
 
 
@@ -54,13 +55,13 @@ def make_model(args, dev, precision="bf16"):
     return m.to(dev)
 
 
-def bench_train(args, dev, rank, world):
+def bench_train(args, dev, rank, world, precision="bf16"):
     from smer_music_generation_amd import ops
     from smer_music_generation_amd.synth import synth_training_batch
     from smer_music_generation_amd.train import Trainer
     from smer_music_generation_amd.vocab import WordVocab
     v = WordVocab(0, CTRL)
-    m = make_model(args, dev)
+    m = make_model(args, dev, precision)
     tr = Trainer(m, v, lr=1e-4)
     b = synth_training_batch(1000 + rank, v, args.batch, args.seq, args.tgt)
     bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
@@ -126,16 +127,17 @@ def bench_train(args, dev, rank, world):
     return res
 
 
-def bench_train_c4(args, dev, rank, world):
+def bench_train_c4(args, dev, rank, world, precision):
     """BASELINE.json configs[3] / SURVEY §8 C4 shapes: 12 + 12 layers, d_model
     768, 12 heads, FF 2048, per-GPU B=32 sources of S=2048 and T=512 decoder
-    tokens, dropout 0.1, the full train step in bf16 (the fp8 GEMM kernel is
-    a separate building block, tools/bench_fp8.py)."""
+    tokens, dropout 0.1, the full train step.  precision "fp8": the QKV / FFN /
+    cross-attention forward contractions on the e4m3 MFMA with delayed
+    per-tensor scaling (fp8.py), everything else bf16; "bf16" for comparison."""
     import copy
     a = copy.copy(args)
     a.layers, a.d_model, a.nhead, a.seq, a.tgt = 12, 768, 12, 2048, 512
     a.steps, a.warmup, a.roofline = args.c4_steps, args.c4_warmup, False
-    return bench_train(a, dev, rank, world)
+    return bench_train(a, dev, rank, world, precision)
 
 
 def _infill_requests(n, target_len=1024, seed0=0, n_infill_bars=2):
@@ -404,7 +406,8 @@ def main():
     _lib.load()
 
     tr = bench_train(args, dev, rank, world)
-    c4 = bench_train_c4(args, dev, rank, world) if args.c4 else None
+    c4 = bench_train_c4(args, dev, rank, world, "fp8") if args.c4 else None
+    c4b = bench_train_c4(args, dev, rank, world, "bf16") if args.c4 else None
     inf = None
     if args.infill:
         inf = bench_infill(args, dev, rank)
@@ -467,11 +470,16 @@ def main():
                                                      "(batch 1, default weighted sampling, "
                                                      "KV-cached), tokens/s")},
             "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
-                                          "S=2048 T=512, bf16",
+                                          "S=2048 T=512",
+                                "dtype": "fp8 (e4m3 QKV/FFN/cross forward GEMMs, delayed "
+                                         "scaling; bf16 elsewhere)",
                                 "value": round(c4["tokens_per_s"], 1),
                                 "ms_per_step": round(c4["ms_per_step"], 2),
                                 "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),
-                                "mfma_frac_whole_step": round(c4["mfma_frac_whole_step"], 4),
+                                "frac_of_fp8_peak": round(c4["step_tflops_per_gpu"] / FP8_PEAK_TFLOPS, 4),
+                                "frac_of_bf16_peak": round(c4["mfma_frac_whole_step"], 4),
+                                "bf16_value": c4b and round(c4b["tokens_per_s"], 1),
+                                "bf16_ms_per_step": c4b and round(c4b["ms_per_step"], 2),
                                 "global_batch": args.batch * world, "steps": args.c4_steps,
                                 "parallelism": "dp%d" % world},
             "infill_c5": c5 and {"metric": "C5 batched infill tokens/s (64 requests x ~4096-token "

@@ -45,6 +45,8 @@
  *   smer_cast            fp32 master -> bf16 working copies
  *   smer_fp8_quantize    per-tensor e4m3 quantisation (amax + scaled cast) of
  *                        a bf16 activation / weight for the fp8 GEMM
+ *   smer_gemm_fp8(_q), smer_layernorm_fwd_fp8, smer_fp8_scales: the fp8
+ *                        training forward (delayed per-tensor scaling)
  *   smer_gemm_fp8        fp8 (e4m3 x e4m3, fp32 accumulate) forward Linear of
  *                        the QKV / FFN contractions (BASELINE C4)
  */
@@ -244,6 +246,27 @@ int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, l
                   const float* a_inv, const float* b_inv, const float* bias, int relu,
                   const void* residual, long ldr, float drop_p, uint32_t drop_seed, void* C,
                   long ldc, smer_stream_t stream);
+
+/* fp8 training forward with delayed per-tensor scaling (BASELINE C4, the
+ * QKV / FFN contractions transformer.py:389,393,459,467).  Producers write
+ * an e4m3 copy q8 = e4m3(out * *qs) beside their bf16 output and fold
+ * max|out| into *amax (float bits, atomicMax); qs / inv come from the
+ * previous step's amax via smer_fp8_scales.  smer_gemm_fp8_q is
+ * smer_gemm_fp8 plus such a copy of C (the FFN1 output feeding FFN2);
+ * smer_layernorm_fwd_fp8 is smer_layernorm_fwd (bf16) plus such a copy of y.
+ * smer_fp8_scales: for i < n, qs[i] = 448 / amax_prev[i], inv[i] =
+ * amax_prev[i] / 448 (both 1 when amax_prev is 0), amax_next[i] = 0. */
+int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                    const float* a_inv, const float* b_inv, const float* bias, int relu,
+                    const void* residual, long ldr, float drop_p, uint32_t drop_seed, void* C,
+                    long ldc, void* q8, long ldq8, const float* qs, unsigned* amax,
+                    smer_stream_t stream);
+int smer_layernorm_fwd_fp8(int M, int N, const void* x, long ldx, const float* gamma,
+                           const float* beta, float eps, void* y, long ldy, float* mean,
+                           float* rstd, void* q8, long ldq, const float* qs, unsigned* amax,
+                           smer_stream_t stream);
+int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, float* inv, unsigned* amax_next,
+                    smer_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,11 @@ SIGNATURES = {
     "smer_fp8_quantize": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P]),
     "smer_gemm_fp8": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_int, P, c_long,
                               c_float, c_u32, P, c_long, P]),
+    "smer_gemm_fp8_q": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_int, P,
+                                c_long, c_float, c_u32, P, c_long, P, c_long, P, P, P]),
+    "smer_layernorm_fwd_fp8": (c_int, [c_int, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P,
+                                       c_long, P, P, P]),
+    "smer_fp8_scales": (c_int, [c_int, P, P, P, P, P]),
     "smer_grammar_greedy_step": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P, c_int,
                                          c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
     "smer_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,

@@ -233,3 +233,42 @@ __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+
+// ---- fp8 (OCP e4m3) activations with delayed per-tensor scaling ----------
+// A producer (LayerNorm, the FFN1 epilogue) writes q = e4m3(v * qs) next to
+// its bf16 output, where qs = 448 / amax of the previous step (1 when none),
+// and folds max|v| into this step's amax.  Consumers dequantise with
+// inv = 1 / qs.  amax is kept as float bits (non-negative floats order like
+// unsigned ints, so integer atomicMax is exact and arrival-order free).
+__device__ __forceinline__ uint2 smer_q8x8(const float (&v)[8], float qs) {
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = fminf(fmaxf(v[4 * h + k] * qs, -448.f), 448.f);
+    int p = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    p = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], p, true);
+    w[h] = (uint32_t)p;
+  }
+  return make_uint2(w[0], w[1]);
+}
+__device__ __forceinline__ float smer_absmax8(const float (&v)[8]) {
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(v[k]));
+  return m;
+}
+// wave-wide max, then at most one atomic per wave (every lane must call).
+// amax only grows, so a wave whose max does not exceed the value it reads
+// skips the atomic (a stale read only costs an extra atomic): the producers
+// of one tensor (tens of thousands of waves) would otherwise serialise on
+// one address.
+__device__ __forceinline__ void smer_amax_commit(unsigned* amax, float m) {
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned b = __float_as_uint(m);
+    if (b > __hip_atomic_load(amax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(amax, b);
+  }
+}
+

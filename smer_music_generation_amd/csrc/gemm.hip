@@ -40,6 +40,12 @@ struct GemmEpi {
   const int32_t* kv_req;
   const int32_t* kv_pos;
   int kv_col0;
+  // fp8 copy of the bf16 output (delayed scaling, common.h): q8 = e4m3(out *
+  // *q8_scale); the caller folds max|out| into *q8_amax (vector path only)
+  uint8_t* q8;
+  long ldq8;
+  const float* q8_scale;
+  unsigned* q8_amax;
 };
 
 template <typename T>
@@ -67,9 +73,9 @@ __device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int ro
 
 // Eight consecutive columns of one row (bf16 activations).  Vector path when
 // the host verified 16-B alignment of every operand (e.vec) and the chunk is
-// full; otherwise per element.
+// full; otherwise per element.  amax_acc: running max|out| of the fp8 copy.
 __device__ __forceinline__ void epi_apply8(const GemmEpi& e, int M, int N, int row, int col,
-                                           float (&v)[8]) {
+                                           float (&v)[8], float* amax_acc = nullptr) {
   const int valid = min(8, N - col);
   if (!e.vec || valid < 8) {
     for (int k = 0; k < valid; ++k) epi_apply<bf16>(e, M, N, row, col + k, v[k]);
@@ -103,6 +109,13 @@ __device__ __forceinline__ void epi_apply8(const GemmEpi& e, int M, int N, int r
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
     if (e.C) *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)row * e.ldc + col) = o;
+    if (e.q8 && amax_acc) {  // fp8 copy of the stored bf16 values
+      float r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = (float)o[k];
+      *reinterpret_cast<uint2*>(e.q8 + (long)row * e.ldq8 + col) = smer_q8x8(r, *e.q8_scale);
+      *amax_acc = fmaxf(*amax_acc, smer_absmax8(r));
+    }
     if (e.kv && col >= e.kv_col0)  // kv_col0 % 8 == 0: a chunk is all K/V or all Q
       *reinterpret_cast<bf16x8*>((bf16*)e.kv + (long)e.kv_req[row] * e.kv_req_stride +
                                  (long)e.kv_pos[row] * e.kv_row_stride + (col - e.kv_col0)) = o;
@@ -1342,6 +1355,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   const int nk = K / F8K;
   GemmEpi ee = e;
   ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
+  float amax_acc = 0.f;
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;
@@ -1406,11 +1420,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
         const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
         const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        epi_apply8(ee, M, N, grow, gcol, v);
+        epi_apply8(ee, M, N, grow, gcol, v, &amax_acc);
       }
       __syncthreads();
     }
   }
+  if (e.q8) smer_amax_commit(e.q8_amax, amax_acc);
 }
 
 // amax(|x|) over a [rows, cols] bf16 view: float bits of non-negative values
@@ -1485,10 +1500,25 @@ extern "C" int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, vo
   return SMER_OK;
 }
 
+extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                               const float* a_inv, const float* b_inv, const float* bias, int relu,
+                               const void* residual, long ldr, float drop_p, uint32_t drop_seed,
+                               void* C, long ldc, void* q8, long ldq8, const float* q8_scale,
+                               unsigned* q8_amax, smer_stream_t stream);
+
 extern "C" int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                              const float* a_inv, const float* b_inv, const float* bias, int relu,
                              const void* residual, long ldr, float drop_p, uint32_t drop_seed,
                              void* C, long ldc, smer_stream_t stream) {
+  return smer_gemm_fp8_q(M, N, K, A, lda, B, ldb, a_inv, b_inv, bias, relu, residual, ldr, drop_p,
+                         drop_seed, C, ldc, nullptr, 0, nullptr, nullptr, stream);
+}
+
+extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                               const float* a_inv, const float* b_inv, const float* bias, int relu,
+                               const void* residual, long ldr, float drop_p, uint32_t drop_seed,
+                               void* C, long ldc, void* q8, long ldq8, const float* q8_scale,
+                               unsigned* q8_amax, smer_stream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % G2 || N % G2 || K % F8K)
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm_fp8: needs M, N % 256 == 0 and K % 128 == 0");
   SMER_REQUIRE(A && B && C && a_inv && b_inv, "smer_gemm_fp8: null pointer");
@@ -1502,6 +1532,11 @@ extern "C" int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const
   e.C = C; e.ldc = ldc;
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
   e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc);
+  if (q8) {
+    SMER_REQUIRE(e.vec && q8_scale && q8_amax && (((uintptr_t)q8) & 7) == 0 && ldq8 % 8 == 0,
+                 "smer_gemm_fp8_q: fp8 output needs aligned vectors, scale and amax");
+    e.q8 = (uint8_t*)q8; e.ldq8 = ldq8; e.q8_scale = q8_scale; e.q8_amax = q8_amax;
+  }
   hipStream_t s = (hipStream_t)stream;
   static bool attr_set = false;
   if (!attr_set) {

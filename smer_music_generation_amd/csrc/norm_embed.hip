@@ -34,16 +34,20 @@ template <> struct Vec8<float> {
 };
 }  // namespace
 
-template <typename T>
+// Q8: also the e4m3 copy of y (delayed scaling, common.h) for an fp8 GEMM
+template <typename T, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __restrict__ x, long ldx,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      T* __restrict__ y, long ldy,
                                                      float* __restrict__ mean,
-                                                     float* __restrict__ rstd) {
+                                                     float* __restrict__ rstd,
+                                                     uint8_t* __restrict__ q8 = nullptr, long ldq = 0,
+                                                     const float* __restrict__ qs_p = nullptr,
+                                                     unsigned* __restrict__ amax = nullptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
+  if (row >= M) return;  // wave-uniform: a wave is one row
   const int nch = N >> 3;
   float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, issued before x
 #pragma unroll
@@ -55,6 +59,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
     }
   }
   float v[LNR_MAXC][8], mu, rs;
+  float am = 0.f;
   ln_row_stats<T>(x + (long)row * ldx, N, eps, lane, v, mu, rs);
 #pragma unroll
   for (int c = 0; c < LN_MAXC; ++c) {
@@ -64,8 +69,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gb[c][i], gb[c][8 + i]);
       Vec8<T>::store(y + (long)row * ldy + ch * 8, o);
+      if constexpr (Q8) {
+        // quantise the value the bf16 output holds (what the bf16 path reads)
+        float r[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = (float)(T)o[i];
+        *reinterpret_cast<uint2*>(q8 + (long)row * ldq + ch * 8) = smer_q8x8(r, *qs_p);
+        am = fmaxf(am, smer_absmax8(r));
+      }
     }
   }
+  if constexpr (Q8) smer_amax_commit(amax, am);
   if (lane == 0) {
     if (mean) mean[row] = mu;
     if (rstd) rstd[row] = rs;
@@ -304,6 +318,49 @@ extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long l
   else
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_fwd: dtype");
   SMER_CHECK_LAUNCH("smer_layernorm_fwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_layernorm_fwd_fp8(int M, int N, const void* x, long ldx, const float* gamma,
+                                      const float* beta, float eps, void* y, long ldy, float* mean,
+                                      float* rstd, void* q8, long ldq, const float* qs,
+                                      unsigned* amax, smer_stream_t stream) {
+  SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_fwd_fp8: N % 8 == 0 and N <= 2048");
+  SMER_REQUIRE(ldx % 8 == 0 && ldy % 8 == 0 && ldq % 8 == 0, "smer_layernorm_fwd_fp8: strides % 8");
+  SMER_REQUIRE(q8 && qs && amax && (((uintptr_t)q8) & 7) == 0, "smer_layernorm_fwd_fp8: fp8 output");
+  SMER_REQUIRE((((uintptr_t)gamma | (uintptr_t)beta) & 15) == 0,
+               "smer_layernorm_fwd_fp8: gamma / beta must be 16-B aligned");
+  if (M == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4);
+  hipLaunchKernelGGL((ln_fwd_kernel<bf16, true>), grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma,
+                     beta, eps, (bf16*)y, ldy, mean, rstd, (uint8_t*)q8, ldq, qs, amax);
+  SMER_CHECK_LAUNCH("smer_layernorm_fwd_fp8");
+  return SMER_OK;
+}
+
+// Delayed scaling: per site, the scale of this step from the amax the
+// producers recorded in the previous one (amax_prev), and the next step's
+// amax slot cleared.  qs = 448 / amax, inv = amax / 448 (1 / 1 when zero).
+__global__ void fp8_scales_kernel(int n, const unsigned* __restrict__ amax_prev,
+                                  float* __restrict__ qs, float* __restrict__ inv,
+                                  unsigned* __restrict__ amax_next) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float a = __uint_as_float(amax_prev[i]);
+  const bool ok = a > 0.f && a < 3.0e38f;
+  qs[i] = ok ? 448.f / a : 1.f;
+  inv[i] = ok ? a / 448.f : 1.f;
+  amax_next[i] = 0u;
+}
+
+extern "C" int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, float* inv,
+                               unsigned* amax_next, smer_stream_t stream) {
+  SMER_REQUIRE(n >= 0 && (n == 0 || (amax_prev && qs && inv && amax_next)), "smer_fp8_scales: pointers");
+  if (n == 0) return SMER_OK;
+  hipLaunchKernelGGL(fp8_scales_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n,
+                     amax_prev, qs, inv, amax_next);
+  SMER_CHECK_LAUNCH("smer_fp8_scales");
   return SMER_OK;
 }
 

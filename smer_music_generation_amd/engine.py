@@ -57,10 +57,11 @@ class Engine:
         self._wgen = 0          # bumped whenever the working weights are rewritten
         self._ckv_all = None    # (key, W [L*2d, d], b [L*2d]) stacked cross-attn K/V projections
         self._side = {}         # device -> (wgrad stream, its split-K workspace)
+        self._fp8 = None        # fp8.Fp8Forward (precision "fp8")
 
     # ------------------------------------------------------------------
     def act_dtype(self):
-        return torch.bfloat16 if self.m.precision == "bf16" else torch.float32
+        return torch.float32 if self.m.precision == "fp32" else torch.bfloat16
 
     def _weights_flat(self, dt):
         flat = self.m.flat_parameters()
@@ -218,6 +219,43 @@ class Engine:
         ops.layernorm(x, wb[0], wb[1], y, mean, rstd)
         return y, mean, rstd
 
+    # ---- fp8 forward helpers (precision "fp8"; see fp8.py) --------------
+    def _ln_q(self, f8, x, wb, dt, site):
+        """LayerNorm; with f8, also the e4m3 copy of y for an fp8 GEMM.
+        Returns (y, mean, rstd, (y8, site index) or None)."""
+        if f8 is None or site is None:
+            return self._ln(x, wb, dt) + (None,)
+        M, N = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(M, device=x.device)
+        rstd = torch.empty(M, device=x.device)
+        si = f8.site(site)
+        q = torch.empty(M, N, dtype=torch.uint8, device=x.device)
+        ops.layernorm_fp8(x, wb[0], wb[1], y, mean, rstd, q, f8.qs_of(si), f8.amax_of(si))
+        return y, mean, rstd, (q, si)
+
+    def _lin(self, f8, x, xq, wname, w, b, q_site=None, **epi):
+        """x @ w^T + epilogue: on the fp8 MFMA when x has an e4m3 copy xq and
+        the shape tiles, else bf16.  q_site: also write the e4m3 copy of the
+        output (returns (out, (q, site)))."""
+        M, K = x.shape
+        N = w.shape[0]
+        if f8 is not None and xq is not None:
+            from .fp8 import eligible
+            if eligible(M, N, K) and epi.get("gate") is None:
+                w8, winv = f8.weight(wname, w)
+                out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+                if q_site is not None:
+                    si = f8.site(q_site)
+                    q = torch.empty(M, N, dtype=torch.uint8, device=x.device)
+                    ops.gemm_fp8_q(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, q8=q,
+                                   qs=f8.qs_of(si), amax=f8.amax_of(si), **epi)
+                    return out, (q, si)
+                ops.gemm_fp8(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, **epi)
+                return out
+        out = ops.linear(x, w, b, **epi)
+        return (out, None) if q_site is not None else out
+
     def forward(self, src, tgt, src_kpm, tgt_kpm, mem_kpm, *, training, need_weights, save,
                 seed=0):
         """Returns (logits fp32 [B*T, V], weights [L,B,T,S] or None, ctx)."""
@@ -256,24 +294,35 @@ class Engine:
             ctx.masks[key] = m_
             return m_
 
+        f8 = None
+        if m.precision == "fp8":
+            if self._fp8 is None:
+                from .fp8 import Fp8Forward
+                self._fp8 = Fp8Forward(self, dev)
+            f8 = self._fp8
+            f8.begin()
         x = torch.empty(B * S, d, dtype=dt, device=dev)
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
+        xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)
         for i, L in enumerate(W.enc):
-            qkv = ops.linear(x, L.in_w, L.in_b)
+            qkv = self._lin(f8, x, xq, "enc%d.in" % i, L.in_w, L.in_b)
             o = torch.empty(B * S, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, S, device=dev)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
                          D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)),
                          drop_mask=amask(("enc", i), S, S))
             y1 = ops.linear(o, L.out_w, L.out_b, residual=x, drop_p=p_tr, seed=sd(_site("enc", i, 1)))
-            x1, m1, r1 = self._ln(y1, L.n1, dt)
-            h = ops.linear(x1, L.l1_w, L.l1_b, relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
-            y2 = ops.linear(h, L.l2_w, L.l2_b, residual=x1, drop_p=p_tr, seed=sd(_site("enc", i, 3)))
-            x2, m2, r2 = self._ln(y2, L.n2, dt)
+            x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "enc%d.ln1" % i)
+            h, hq = self._lin(f8, x1, x1q, "enc%d.l1" % i, L.l1_w, L.l1_b, q_site="enc%d.h" % i,
+                              relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
+            y2 = self._lin(f8, h, hq, "enc%d.l2" % i, L.l2_w, L.l2_b, residual=x1, drop_p=p_tr,
+                           seed=sd(_site("enc", i, 3)))
+            x2, m2, r2, xq = self._ln_q(f8, y2, L.n2, dt,
+                                        "enc%d.ln2" % i if i + 1 < self.n_enc else None)
             if save:
                 ctx.enc.append((x, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2))
             x = x2
-        mem, me, re = self._ln(x, W.enc_norm, dt)
+        mem, me, re, memq = self._ln_q(f8, x, W.enc_norm, dt, "mem")
         ctx.enc_last = (x, me, re)
         ctx.mem = mem
 
@@ -281,17 +330,18 @@ class Engine:
         ops.embed(tgt_ids, W.emb, pe2, y, L=T, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_tgt"]))
         wts = torch.empty(self.n_dec, B, T, S, device=dev) if need_weights else None
         # every decoder layer's cross-attention K|V of the memory, one GEMM
-        kvc_all = ops.linear(mem, W.ckv_all, W.ckv_b_all) if self.n_dec else None
+        kvc_all = self._lin(f8, mem, memq, "ckv", W.ckv_all, W.ckv_b_all) if self.n_dec else None
+        yq = None
         for i, L in enumerate(W.dec):
-            qkv = ops.linear(y, L.sa_w, L.sa_b)
+            qkv = self._lin(f8, y, yq, "dec%d.sa" % i, L.sa_w, L.sa_b)
             o = torch.empty(B * T, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, T, device=dev)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
                          D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)),
                          drop_mask=amask(("dec", i), T, T))
             y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr, seed=sd(_site("dec", i, 1)))
-            x1, m1, r1 = self._ln(y1, L.n1, dt)
-            qc = ops.linear(x1, L.cq_w, L.cq_b)
+            x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "dec%d.ln1" % i)
+            qc = self._lin(f8, x1, x1q, "dec%d.cq" % i, L.cq_w, L.cq_b)
             kvc = kvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             oc = torch.empty(B * T, d, dtype=dt, device=dev)
             lsec = torch.empty(B, H, T, device=dev)
@@ -302,10 +352,13 @@ class Engine:
                 ops.attn_weights(qc, kvc[:, :d], lsec, wts[i], B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                                  scale=scale)
             y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1, drop_p=p_tr, seed=sd(_site("dec", i, 3)))
-            x2, m2, r2 = self._ln(y2, L.n2, dt)
-            h = ops.linear(x2, L.l1_w, L.l1_b, relu=True, drop_p=p_tr, seed=sd(_site("dec", i, 4)))
-            y3 = ops.linear(h, L.l2_w, L.l2_b, residual=x2, drop_p=p_tr, seed=sd(_site("dec", i, 5)))
-            x3, m3, r3 = self._ln(y3, L.n3, dt)
+            x2, m2, r2, x2q = self._ln_q(f8, y2, L.n2, dt, "dec%d.ln2" % i)
+            h, hq = self._lin(f8, x2, x2q, "dec%d.l1" % i, L.l1_w, L.l1_b, q_site="dec%d.h" % i,
+                              relu=True, drop_p=p_tr, seed=sd(_site("dec", i, 4)))
+            y3 = self._lin(f8, h, hq, "dec%d.l2" % i, L.l2_w, L.l2_b, residual=x2, drop_p=p_tr,
+                           seed=sd(_site("dec", i, 5)))
+            x3, m3, r3, yq = self._ln_q(f8, y3, L.n3, dt,
+                                        "dec%d.ln3" % i if i + 1 < self.n_dec else None)
             if save:
                 ctx.dec.append((y, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2,
                                 h, y3, m3, r3))

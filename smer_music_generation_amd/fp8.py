@@ -1,0 +1,88 @@
+"""fp8 (OCP e4m3) training forward with delayed per-tensor scaling.
+
+BASELINE.json configs[3] (C4) asks for fp8 MFMA GEMMs on CDNA4.  In the
+`precision="fp8"` mode the forward contractions whose input comes from a
+LayerNorm or from the FFN1 epilogue run on the block-scaled fp8 MFMA
+(`smer_gemm_fp8`): the QKV in-projections of layers >= 1, FFN1, FFN2, the
+decoder's cross-attention Q and the stacked cross-attention K/V of the memory
+(`transformer.py:389,393,459,463,467`).  Out-projections (input: attention
+output), the vocab head and every backward GEMM stay bf16; master weights fp32,
+working weights bf16.
+
+Scaling (no standalone quantise pass over activations):
+  * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy
+    q = e4m3(y * qs) beside its bf16 output and folds max|y| into an amax
+    slot of this forward (atomicMax on float bits);
+  * qs for forward t comes from the amax recorded in forward t-1
+    (`smer_fp8_scales`: qs = 448 / amax, inv = amax / 448; 1 / 1 for the
+    first forward, which suits LayerNorm / ReLU outputs of O(1));
+  * weights are quantised once per optimizer step (current scaling, one
+    amax + cast pair per weight matrix) and cached until the next update.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+N_SITES = 512
+
+
+class Fp8Forward:
+    def __init__(self, engine, device):
+        self.eng = engine
+        self.dev = device
+        self.sites = {}
+        self.amax = [torch.zeros(N_SITES, dtype=torch.int32, device=device) for _ in range(2)]
+        self.qs = torch.ones(N_SITES, device=device)
+        self.inv = torch.ones(N_SITES, device=device)
+        self.t = 0
+        self.cur = self.amax[1]
+        self._wkey = None
+        self._w = {}
+
+    def begin(self):
+        """Start a forward: this forward's scales from the previous one's amax."""
+        prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
+        ops.fp8_scales(prev, self.qs, self.inv, nxt)
+        self.cur = nxt
+        self.t += 1
+
+    def site(self, name):
+        i = self.sites.get(name)
+        if i is None:
+            i = len(self.sites)
+            if i >= N_SITES:
+                raise RuntimeError("fp8: more than %d scaled activations" % N_SITES)
+            self.sites[name] = i
+        return i
+
+    def qs_of(self, i):
+        return self.qs[i:i + 1]
+
+    def inv_of(self, i):
+        return self.inv[i:i + 1]
+
+    def amax_of(self, i):
+        return self.cur[i:i + 1]
+
+    def weight(self, name, w):
+        """(e4m3 copy, inv scale) of a bf16 working weight, refreshed whenever
+        the engine's weights change (after every optimizer step)."""
+        key = self.eng._wgen
+        if key != self._wkey:
+            self._w = {}
+            self._wkey = key
+        hit = self._w.get(name)
+        if hit is None or hit[0].shape != w.shape:
+            q = torch.empty(w.shape, dtype=torch.uint8, device=w.device)
+            inv = torch.empty(1, device=w.device)
+            ops.fp8_quantize(w, q, inv)
+            hit = (q, inv)
+            self._w[name] = hit
+        return hit
+
+
+def eligible(M, N, K):
+    """Shapes the fp8 MFMA kernel tiles (256 x 256 outputs, 128-deep K)."""
+    return M % 256 == 0 and N % 256 == 0 and K % 128 == 0

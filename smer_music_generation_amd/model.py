@@ -198,7 +198,9 @@ class ScoreTransformer(nn.Module):
     """`model.py:59-106`.
 
     Extra keyword-only knobs (reference defaults preserved):
-      precision: 'bf16' (MFMA path, default) or 'fp32' (parity path)
+      precision: 'bf16' (MFMA path, default), 'fp32' (parity path) or 'fp8'
+        (the QKV / FFN / cross-attention forward contractions on the e4m3
+        MFMA with delayed per-tensor scaling, everything else bf16; fp8.py)
       need_weights: return the head-averaged cross-attention weights
         [B, L, T, S] like the reference (default True); False returns None.
     """
@@ -281,7 +283,7 @@ class ScoreTransformer(nn.Module):
         return g
 
     def set_precision(self, precision):
-        assert precision in ("bf16", "fp32")
+        assert precision in ("bf16", "fp32", "fp8")
         self.precision = precision
         return self
 

@@ -300,10 +300,54 @@ def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None,
     N = b8.shape[0]
     if M % 256 or N % 256 or K % 128:
         return False
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     call("smer_gemm_fp8", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
          _p(bias), int(bool(relu)), _p(residual), _ld(residual) if residual is not None else 0,
          float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out), _stream())
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * K, "fp8 M%d N%d K%d%s" % (
+            M, N, K, " R" if residual is not None else "")))
     return True
+
+
+def gemm_fp8_q(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
+               seed=0, q8=None, qs=None, amax=None):
+    """gemm_fp8 plus an e4m3 copy of `out` (q8 = e4m3(out * qs), max|out| folded
+    into amax): the fp8 training forward's FFN1 (its output feeds FFN2)."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    if M % 256 or N % 256 or K % 128:
+        return False
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    call("smer_gemm_fp8_q", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
+         _p(bias), int(bool(relu)), _p(residual), _ld(residual) if residual is not None else 0,
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out), _p(q8),
+         _ld(q8) if q8 is not None else 0, _p(qs), _p(amax), _stream())
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * K, "fp8q M%d N%d K%d" % (M, N, K)))
+    return True
+
+
+def layernorm_fp8(x, gamma, beta, y, mean, rstd, q8, qs, amax, eps=1e-5):
+    """bf16 LayerNorm that also writes the e4m3 copy of y (delayed scaling)."""
+    M, N = x.shape
+    call("smer_layernorm_fwd_fp8", M, N, _p(x), _ld(x), _p(gamma), _p(beta), float(eps), _p(y),
+         _ld(y), _p(mean), _p(rstd), _p(q8), _ld(q8), _p(qs), _p(amax), _stream())
+
+
+def fp8_scales(amax_prev, qs, inv, amax_next):
+    call("smer_fp8_scales", amax_prev.numel(), _p(amax_prev), _p(qs), _p(inv), _p(amax_next),
+         _stream())
 
 
 def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, out_tok, alive, *,

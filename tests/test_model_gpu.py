@@ -301,7 +301,7 @@ def test_device_grammar_matches_host_loop(golden_dir, precision):
             assert [str(x) for x in got[0]] == rec["restored"]
 
 
-@pytest.mark.parametrize("precision,ltol,ptol", [("fp32", 1e-4, 1e-5), ("bf16", 3e-2, 2e-3)])
+@pytest.mark.parametrize("precision,ltol,ptol", [("fp32", 1e-4, 1e-3), ("bf16", 3e-2, 0.1)])
 def test_three_fused_steps_track_oracle(precision, ltol, ptol):
     """Three Trainer steps (fused CE + backward + fused Adam) vs three oracle
     steps (reference autograd + torch Adam): the weights the 2nd / 3rd
@@ -326,6 +326,7 @@ def test_three_fused_steps_track_oracle(precision, ltol, ptol):
     tr = Trainer(m, v, lr=lr, eps=eps)
     bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
     params = {k: t for k, t in sd.items() if k != "pos_enc.pe"}
+    p0 = {k: t.clone().numpy() for k, t in params.items()}
     mo = {k: torch.zeros_like(t) for k, t in params.items()}
     vo = {k: torch.zeros_like(t) for k, t in params.items()}
     losses = []
@@ -338,6 +339,10 @@ def test_three_fused_steps_track_oracle(precision, ltol, ptol):
     for got, ref in losses:
         assert abs(got - ref) < ltol * max(1, ref), losses
     assert losses[2][1] < losses[0][1] - 1e-3, losses  # the steps move the loss
+    # the change of every parameter over the three steps (lr * accumulated
+    # gradient terms) vs the reference change
     for name, p in m.named_parameters():
-        err = fro_rel(p.detach().cpu().numpy(), params[name].numpy())
+        got = p.detach().cpu().numpy() - p0[name]
+        ref = params[name].numpy() - p0[name]
+        err = fro_rel(got, ref)
         assert err < ptol, (name, err)
