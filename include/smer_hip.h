@@ -242,6 +242,13 @@ int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, in
 size_t smer_fp8_quantize_workspace(void);
 int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, void* q, long ldq,
                       void* workspace, float* inv_scale, smer_stream_t stream);
+/* Batched smer_fp8_quantize over nseg contiguous bf16 tensors: seg is a
+ * DEVICE array of nseg x 3 int64 (src bf16*, dst uint8*, n elements; n % 8
+ * == 0, src 16-B / dst 8-B aligned); amax_ws: nseg uints of workspace;
+ * inv_scale[s] = amax_s / 448.  Same numerics as one smer_fp8_quantize per
+ * tensor (per-tensor current scaling); blocks_per_seg: grid.x per tensor. */
+int smer_fp8_quantize_segments(int nseg, const int64_t* seg, unsigned* amax_ws, float* inv_scale,
+                               int blocks_per_seg, smer_stream_t stream);
 int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                   const float* a_inv, const float* b_inv, const float* bias, int relu,
                   const void* residual, long ldr, float drop_p, uint32_t drop_seed, void* C,

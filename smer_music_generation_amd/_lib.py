@@ -46,6 +46,7 @@ SIGNATURES = {
                                    P, c_long, P, c_long, P, c_long, c_long, P, P, c_int, P]),
     "smer_fp8_quantize_workspace": (c_size, []),
     "smer_fp8_quantize": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P]),
+    "smer_fp8_quantize_segments": (c_int, [c_int, P, P, P, c_int, P]),
     "smer_gemm_fp8": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_int, P, c_long,
                               c_float, c_u32, P, c_long, P]),
     "smer_gemm_fp8_q": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_int, P,

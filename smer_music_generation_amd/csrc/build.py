@@ -4,6 +4,8 @@
 
 Each .hip/.cpp is compiled to an object under csrc/_build/ (skipped when
 up to date) and linked into smer_music_generation_amd/libsmer_hip.so.
+The host-only data pipeline loop (dataset.cpp, include/smer_data.h) is built
+with g++ into smer_music_generation_amd/libsmer_data.so.
 """
 from __future__ import annotations
 
@@ -17,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
 OUT = os.path.join(PKG, "libsmer_hip.so")
+DATA_OUT = os.path.join(PKG, "libsmer_data.so")
 OBJ = os.path.join(HERE, "_build")
 SOURCES = ["abi.cpp", "gemm.hip", "attention.hip", "norm_embed.hip", "train_ops.hip", "decode_ops.hip"]
 HEADERS = ["common.h", os.path.join("..", "..", "include", "smer_hip.h")]
@@ -54,7 +57,26 @@ def _compile(src):
     return obj
 
 
+def build_data(verbose=True):
+    """libsmer_data.so: host C++ only (g++), no ROCm needed."""
+    src = os.path.join(HERE, "dataset.cpp")
+    hdr = os.path.join(ROOT, "include", "smer_data.h")
+    if _newer(DATA_OUT, [src, hdr]):
+        cxx = os.environ.get("CXX") or shutil.which("g++") or shutil.which("c++")
+        if not cxx:
+            raise RuntimeError("no host C++ compiler (g++) for libsmer_data.so")
+        cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-I" + os.path.join(ROOT, "include"),
+               src, "-o", DATA_OUT]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("g++ failed for dataset.cpp:\n%s\n%s" % (" ".join(cmd), r.stderr))
+    if verbose:
+        print("built", DATA_OUT)
+    return DATA_OUT
+
+
 def build(verbose=True):
+    build_data(verbose)
     os.makedirs(OBJ, exist_ok=True)
     jobs = min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:

@@ -612,6 +612,83 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int
 }
 }  // namespace
 
+// Streamed epilogue of the 256 x 256 kernels (bf16 and fp8): the residual /
+// gate tile of pass p is DMA'd into LDS (slot A for even passes, B for odd)
+// one pass ahead, so the passes no longer pay a dependent HBM round trip
+// each; the bias is in registers (a thread always owns the same 8 columns).
+// The caller DMA'd the X rows of pass 0 into slot A during its K loop.
+// Q8: also the e4m3 copy of the stored values (fp8 training forward).
+template <bool Q8>
+__device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (&acc)[8][4], char* smem,
+                                                 int m0, int n0, int tid, const float (&bv)[8],
+                                                 const bf16* xsrc, long ldx, float& amax_acc) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, c16 = lane & 15;
+  constexpr int EP_LD = G2 + 4;
+  float* ep = reinterpret_cast<float*>(smem);
+  float q8s = 1.f;
+  if constexpr (Q8) q8s = *e.q8_scale;
+  if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid);
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    if (wm == (pass >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = 4 * (pass & 1) + ii;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+      }
+    }
+    __syncthreads();  // ep rows written; X(pass) landed; X(pass-1) slot free
+    if (xsrc && pass >= 1 && pass < 3)
+      g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
+    const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
+    const int ch = tid & 31;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int row = (tid >> 5) + 16 * c;
+      const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
+      float v[8];
+      const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+      const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + bv[k];
+      if (e.relu) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+      }
+      if (e.drop_thr)
+        smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
+      if (xsrc) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
+        if (e.residual) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += (float)xv[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = (float)xv[k] > 0.f ? v[k] * e.gate_scale : 0.f;
+        }
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+      *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+      if constexpr (Q8) {  // e4m3 copy of the stored (bf16-rounded) values
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = (float)o[k];
+        *reinterpret_cast<uint2*>(e.q8 + (long)grow * e.ldq8 + gcol) = smer_q8x8(v, q8s);
+        amax_acc = fmaxf(amax_acc, smer_absmax8(v));
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <bool AK, bool BKC, bool FAST>
 __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int K,
                                                               const bf16* __restrict__ A, long lda,
@@ -691,62 +768,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
     constexpr int EP_LD = G2 + 4;
     float* ep = reinterpret_cast<float*>(smem);
     if constexpr (FAST) {
-      // Streamed epilogue: the residual / gate tile of pass p is DMA'd into
-      // LDS (slot A for even passes, B for odd) one pass ahead, so the
-      // passes no longer pay a dependent HBM round trip each; the bias is in
-      // registers (a thread always owns the same 8 columns).
-      if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid);
-#pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
-        if (wm == (pass >> 1)) {
-#pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            const int i = 4 * (pass & 1) + ii;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
-          }
-        }
-        __syncthreads();  // ep rows written; X(pass) landed; X(pass-1) slot free
-        if (xsrc && pass >= 1 && pass < 3)
-          g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
-        const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
-        const int ch = tid & 31;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int row = (tid >> 5) + 16 * c;
-          const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
-          float v[8];
-          const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
-          const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
-          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + bv[k];
-          if (e.relu) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
-          }
-          if (e.drop_thr)
-            smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
-          if (xsrc) {
-            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
-            if (e.residual) {
-#pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] += (float)xv[k];
-            } else {
-#pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] = (float)xv[k] > 0.f ? v[k] * e.gate_scale : 0.f;
-            }
-          }
-          bf16x8 o;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
-        }
-        __syncthreads();
-      }
+      float amax_unused = 0.f;
+      g2_fast_epilogue<false>(e, acc, smem, m0, n0, tid, bv, xsrc, ldx, amax_unused);
       continue;
     }
 
@@ -1309,6 +1332,14 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 namespace {
 constexpr int F8K = 128;  // K per stage (bytes per row)
 
+// Row swizzle of the 16-B chunks: physical chunk = logical ^ f8_swz(row).
+// A fragment read (ds_read_b128 x 2) is serviced in lane groups of 16 that
+// mix two logical chunks (g and g + 1 of the 16x16x128 layout) over 16 rows;
+// h(r) = bit1(r) | bit2(r) << 2 sends every group's 16 x 16 B to distinct
+// bank quads (the bf16 kernel's (row & 7) swizzle gives 2-way conflicts
+// here: SQ_LDS_BANK_CONFLICT / IDX_ACTIVE measured 0.475).
+__device__ __forceinline__ int f8_swz(int row) { return ((row >> 1) & 1) | (row & 4); }
+
 __device__ __forceinline__ void f8_glds(char* buf, const uint8_t* P, long ld, int rows, int r0,
                                         int k0, int tid) {
   typedef __attribute__((address_space(1))) void gvoid;
@@ -1318,7 +1349,7 @@ __device__ __forceinline__ void f8_glds(char* buf, const uint8_t* P, long ld, in
   for (int c = 0; c < 4; ++c) {
     const int chunk = wave * 4 + c;  // 32 x 1 KiB = 256 rows x 128 B
     const int row = chunk * 8 + (lane >> 3);
-    const int lc = (lane & 7) ^ (row & 7);
+    const int lc = (lane & 7) ^ f8_swz(row);
     const uint8_t* src = P + (long)min(r0 + row, rows - 1) * ld + k0 + lc * 16;
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
   }
@@ -1326,8 +1357,9 @@ __device__ __forceinline__ void f8_glds(char* buf, const uint8_t* P, long ld, in
 // lane (c16, g): row rbase + c16, k bytes [32g, 32g + 32) = chunks 2g, 2g + 1
 __device__ __forceinline__ i32x8 f8_frag(const char* buf, int rbase, int lane) {
   const int g = lane >> 4, row = rbase + (lane & 15);
-  const uint4 lo = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g) ^ (row & 7)) << 4));
-  const uint4 hi = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g + 1) ^ (row & 7)) << 4));
+  const int h = f8_swz(row);
+  const uint4 lo = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g) ^ h) << 4));
+  const uint4 hi = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g + 1) ^ h) << 4));
   return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 }
 __device__ __forceinline__ f32x4 mfma_f8(i32x8 a, i32x8 b, f32x4 c) {
@@ -1335,6 +1367,10 @@ __device__ __forceinline__ f32x4 mfma_f8(i32x8 a, i32x8 b, f32x4 c) {
 }
 }  // namespace
 
+// FAST: the streamed epilogue (e.vec: 16-B aligned vectors; LDS G2_LDS);
+// Q8: also write the e4m3 copy of the output (launched with the generic
+// epilogue: the streamed one spills 37 VGPRs with it and measured slower).
+template <bool FAST, bool Q8>
 __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K,
                                                              const uint8_t* __restrict__ A, long lda,
                                                              const uint8_t* __restrict__ B, long ldb,
@@ -1356,6 +1392,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   GemmEpi ee = e;
   ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
   float amax_acc = 0.f;
+  const bf16* xsrc = (const bf16*)e.residual;
+  const long ldx = e.ldr;
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;
@@ -1371,10 +1409,19 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // FAST: bias columns
+    if (FAST && e.bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8 + 4);
+      bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+      bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+    }
     f8_glds(smem, A, lda, M, m0, 0, tid);
     f8_glds(smem + G2_OP, B, ldb, N, n0, 0, tid);
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // stage kt landed; stage kt-1 fully read
+      // X rows of the first epilogue pass into slot A (beyond the stages)
+      if (FAST && xsrc && kt == nk / 2) g2_xload(smem + G2_XA, xsrc, ldx, m0, n0, tid);
       if (kt + 1 < nk) {
         char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
         f8_glds(nb, A, lda, M, m0, (kt + 1) * F8K, tid);
@@ -1382,21 +1429,41 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
       }
       const char* a_s = smem + (kt & 1) * G2_STAGE;
       const char* b_s = a_s + G2_OP;
-      i32x8 bfr[4];
+      // A fragments run 4 ahead of the MFMAs that use them (a read issued
+      // right before its 4 MFMAs exposes one LDS latency per fragment; all 12
+      // up front does not fit beside the 128 accumulators)
+      constexpr int AHEAD = FAST ? 1 : 3;  // FAST: bias registers leave no room for more
+      i32x8 bfr[4], af[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(b_s, wn * 64 + j * 16, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const i32x8 af = f8_frag(a_s, wm * 128 + i * 16, lane);
+      for (int i = 0; i < AHEAD; ++i) af[i] = f8_frag(a_s, wm * 128 + i * 16, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f8(af, bfr[j], acc[i][j]);
+      for (int i = 0; i < 8; ++i) {
+        if (i + AHEAD < 8) af[i + AHEAD] = f8_frag(a_s, wm * 128 + (i + AHEAD) * 16, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f8(af[i], bfr[j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
 
+    if constexpr (FAST) {
+      g2_fast_epilogue<Q8>(ee, acc, smem, m0, n0, tid, bv, xsrc, ldx, amax_acc);
+      continue;
+    }
     const int g = lane >> 4, c16 = lane & 15;
     constexpr int EP_LD = G2 + 4;
     float* ep = reinterpret_cast<float*>(smem);
+    // the tile's 256 bias values staged in LDS behind the fp32 rows (no
+    // dependent global load per epilogue pass, no extra registers)
+    GemmEpi eb = ee;
+    if (ee.bias) {
+      float* bl = reinterpret_cast<float*>(smem + G2_XB);
+      if (tid < 64) reinterpret_cast<float4*>(bl)[tid] = reinterpret_cast<const float4*>(ee.bias + n0)[tid];
+      eb.bias = bl - n0;
+    }
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
       if (wm == (pass >> 1)) {
@@ -1410,7 +1477,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
               ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
         }
       }
-      __syncthreads();
+      __syncthreads();  // (pass 0: also the bias slice)
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
@@ -1420,12 +1487,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
         const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
         const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        epi_apply8(ee, M, N, grow, gcol, v, &amax_acc);
+        epi_apply8(eb, M, N, grow, gcol, v, &amax_acc);
       }
       __syncthreads();
     }
   }
-  if (e.q8) smer_amax_commit(e.q8_amax, amax_acc);
+  if (Q8) smer_amax_commit(e.q8_amax, amax_acc);
 }
 
 // amax(|x|) over a [rows, cols] bf16 view: float bits of non-negative values
@@ -1477,6 +1544,64 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(int rows, int cols, cons
     }
     *reinterpret_cast<uint2*>(q + r * ldq + c) = make_uint2(w[0], w[1]);
   }
+}
+
+// Batched per-tensor quantisation of many contiguous bf16 tensors (every fp8
+// weight of a model after an optimizer step: 2 launches + 1 memset instead
+// of 3 per tensor).  seg[3 * s] = (src bf16*, dst uint8*, n elements).
+__global__ __launch_bounds__(256) void amax_seg_kernel(const int64_t* __restrict__ seg,
+                                                      unsigned int* __restrict__ amax) {
+  const int s = blockIdx.y;
+  const bf16* x = reinterpret_cast<const bf16*>(seg[3 * s]);
+  const long n8 = seg[3 * s + 2] >> 3;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + 8 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)v[k]));
+  }
+  m = wave_max(m);
+  __shared__ float wm_[4];
+  if ((threadIdx.x & 63) == 0) wm_[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm_[0], wm_[1]), fmaxf(wm_[2], wm_[3]));
+    atomicMax(amax + s, __float_as_uint(m));
+  }
+}
+
+__global__ __launch_bounds__(256) void quant_seg_kernel(const int64_t* __restrict__ seg,
+                                                       const unsigned int* __restrict__ amax,
+                                                       float* __restrict__ inv) {
+  const int s = blockIdx.y;
+  const bf16* x = reinterpret_cast<const bf16*>(seg[3 * s]);
+  uint8_t* q = reinterpret_cast<uint8_t*>(seg[3 * s + 1]);
+  const long n8 = seg[3 * s + 2] >> 3;
+  const float am = __uint_as_float(amax[s]);
+  const float sc = am > 0.f ? 448.f / am : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) inv[s] = 1.f / sc;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + 8 * i);
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = (float)v[k];
+    *reinterpret_cast<uint2*>(q + 8 * i) = smer_q8x8(f, sc);
+  }
+}
+
+extern "C" int smer_fp8_quantize_segments(int nseg, const int64_t* seg, unsigned* amax_ws, float* inv_scale,
+                                          int blocks_per_seg, smer_stream_t stream) {
+  SMER_REQUIRE(nseg >= 0 && nseg <= 65535 && blocks_per_seg > 0, "smer_fp8_quantize_segments: sizes");
+  if (nseg == 0) return SMER_OK;
+  SMER_REQUIRE(seg && amax_ws && inv_scale, "smer_fp8_quantize_segments: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(amax_ws, 0, sizeof(unsigned) * nseg, s) != hipSuccess)
+    return smer_set_error(SMER_ERR_HIP, "smer_fp8_quantize_segments: memset");
+  const dim3 grid(blocks_per_seg, nseg);
+  hipLaunchKernelGGL(amax_seg_kernel, grid, dim3(256), 0, s, seg, amax_ws);
+  hipLaunchKernelGGL(quant_seg_kernel, grid, dim3(256), 0, s, seg, (const unsigned*)amax_ws, inv_scale);
+  SMER_CHECK_LAUNCH("smer_fp8_quantize_segments");
+  return SMER_OK;
 }
 
 extern "C" size_t smer_fp8_quantize_workspace(void) { return 16; }
@@ -1540,14 +1665,25 @@ extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, con
   hipStream_t s = (hipStream_t)stream;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm256_fp8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        2 * G2_STAGE);
+    hipFuncSetAttribute((const void*)gemm256_fp8_kernel<false, false>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G2_STAGE);
+    hipFuncSetAttribute((const void*)gemm256_fp8_kernel<true, false>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+    hipFuncSetAttribute((const void*)gemm256_fp8_kernel<false, true>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G2_STAGE);
     attr_set = true;
   }
   const long tiles = (long)(M / G2) * (N / G2);
   const int grid = tiles > smer_num_cus() ? (smer_num_cus() & ~7) : (int)tiles;
-  hipLaunchKernelGGL(gemm256_fp8_kernel, dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
-                     (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  if (!e.vec)  // (q8 requires e.vec)
+    hipLaunchKernelGGL((gemm256_fp8_kernel<false, false>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N,
+                       K, (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  else if (q8)
+    hipLaunchKernelGGL((gemm256_fp8_kernel<false, true>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
+                       (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  else
+    hipLaunchKernelGGL((gemm256_fp8_kernel<true, false>), dim3(grid), dim3(512), G2_LDS, s, M, N, K,
+                       (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
   SMER_CHECK_LAUNCH("smer_gemm_fp8");
   return SMER_OK;
 }

@@ -46,8 +46,6 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
                                                      const float* __restrict__ qs_p = nullptr,
                                                      unsigned* __restrict__ amax = nullptr) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;  // wave-uniform: a wave is one row
   const int nch = N >> 3;
   float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, issued before x
 #pragma unroll
@@ -58,8 +56,12 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
       Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
     }
   }
-  float v[LNR_MAXC][8], mu, rs;
   float am = 0.f;
+  // a wave is one row (wave-uniform loop; the grid covers M once except in
+  // the Q8 form, whose capped grid loops so that the amax of the whole
+  // tensor is committed by <= 2048 workgroups instead of one atomic per row)
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
+  float v[LNR_MAXC][8], mu, rs;
   ln_row_stats<T>(x + (long)row * ldx, N, eps, lane, v, mu, rs);
 #pragma unroll
   for (int c = 0; c < LN_MAXC; ++c) {
@@ -79,10 +81,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
       }
     }
   }
-  if constexpr (Q8) smer_amax_commit(amax, am);
   if (lane == 0) {
     if (mean) mean[row] = mu;
     if (rstd) rstd[row] = rs;
+  }
+  }
+  if constexpr (Q8) {
+    __shared__ float wam[4];
+    am = wave_max(am);
+    if (lane == 0) wam[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x < 64) smer_amax_commit(amax, lane < 4 ? wam[lane] : 0.f);
   }
 }
 
@@ -332,7 +341,7 @@ extern "C" int smer_layernorm_fwd_fp8(int M, int N, const void* x, long ldx, con
                "smer_layernorm_fwd_fp8: gamma / beta must be 16-B aligned");
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  dim3 grid((M + 3) / 4);
+  dim3 grid(std::min((M + 3) / 4, 2048));
   hipLaunchKernelGGL((ln_fwd_kernel<bf16, true>), grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma,
                      beta, eps, (bf16*)y, ldy, mean, rstd, (uint8_t*)q8, ldq, qs, amax);
   SMER_CHECK_LAUNCH("smer_layernorm_fwd_fp8");

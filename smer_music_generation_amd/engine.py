@@ -157,8 +157,12 @@ class Engine:
         key = (dt, work.data_ptr(), self._wgen, self._version_key())
         if self.n_dec and (self._ckv_all is None or self._ckv_all[0] != key):
             n2 = 2 * d
-            wall = torch.empty(self.n_dec * n2, d, dtype=dt, device=work.device)
-            ball = torch.empty(self.n_dec * n2, device=work.device)
+            if self._ckv_all is not None and self._ckv_all[1].dtype == dt and \
+                    self._ckv_all[1].device == work.device and self._ckv_all[1].shape[0] == self.n_dec * n2:
+                wall, ball = self._ckv_all[1], self._ckv_all[2]  # rewritten in place (stable pointers)
+            else:
+                wall = torch.empty(self.n_dec * n2, d, dtype=dt, device=work.device)
+                ball = torch.empty(self.n_dec * n2, device=work.device)
             for i, L in enumerate(W.dec):
                 ops.cast2d(L.ckv_w, wall[i * n2:(i + 1) * n2])
                 ops.cast(L.ckv_b, ball[i * n2:(i + 1) * n2])
@@ -300,7 +304,7 @@ class Engine:
                 from .fp8 import Fp8Forward
                 self._fp8 = Fp8Forward(self, dev)
             f8 = self._fp8
-            f8.begin()
+            f8.begin(W)
         x = torch.empty(B * S, d, dtype=dt, device=dev)
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
         xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)

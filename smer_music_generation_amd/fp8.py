@@ -16,8 +16,10 @@ Scaling (no standalone quantise pass over activations):
   * qs for forward t comes from the amax recorded in forward t-1
     (`smer_fp8_scales`: qs = 448 / amax, inv = amax / 448; 1 / 1 for the
     first forward, which suits LayerNorm / ReLU outputs of O(1));
-  * weights are quantised once per optimizer step (current scaling, one
-    amax + cast pair per weight matrix) and cached until the next update.
+  * weights are quantised once per optimizer step (current scaling: amax of
+    the new weights, then the cast), all of them in one batched call
+    (`smer_fp8_quantize_segments`: a memset + 2 launches per step), into
+    persistent e4m3 buffers, and reused until the next update.
 """
 from __future__ import annotations
 
@@ -40,13 +42,52 @@ class Fp8Forward:
         self.cur = self.amax[1]
         self._wkey = None
         self._w = {}
+        self._wbuf = {}       # name -> (e4m3 buffer, inv view), persistent
+        self._seg = None      # (key, device seg table, amax workspace, inv)
 
-    def begin(self):
-        """Start a forward: this forward's scales from the previous one's amax."""
+    def begin(self, W=None):
+        """Start a forward: this forward's scales from the previous one's
+        amax; after a weight update, re-quantise every fp8 weight of W."""
         prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
         ops.fp8_scales(prev, self.qs, self.inv, nxt)
         self.cur = nxt
         self.t += 1
+        if W is not None and self.eng._wgen != self._wkey:
+            self._quantize_weights(W)
+
+    @staticmethod
+    def gemm_weights(W):
+        """(name, bf16 weight) of every GEMM that runs on the fp8 MFMA."""
+        out = []
+        for i, L in enumerate(W.enc):
+            out += [("enc%d.in" % i, L.in_w), ("enc%d.l1" % i, L.l1_w), ("enc%d.l2" % i, L.l2_w)]
+        for i, L in enumerate(W.dec):
+            out += [("dec%d.sa" % i, L.sa_w), ("dec%d.cq" % i, L.cq_w), ("dec%d.l1" % i, L.l1_w),
+                    ("dec%d.l2" % i, L.l2_w)]
+        if getattr(W, "ckv_all", None) is not None:
+            out.append(("ckv", W.ckv_all))
+        return out
+
+    def _quantize_weights(self, W):
+        ws = [(n, w) for n, w in self.gemm_weights(W) if w.is_contiguous() and w.numel() % 8 == 0]
+        key = tuple((n, w.data_ptr(), w.numel()) for n, w in ws)
+        if self._seg is None or self._seg[0] != key:
+            rows = []
+            for n, w in ws:
+                buf = self._wbuf.get(n)
+                if buf is None or buf.shape != w.shape:
+                    buf = torch.empty(w.shape, dtype=torch.uint8, device=self.dev)
+                    self._wbuf[n] = buf
+                rows.append((w.data_ptr(), buf.data_ptr(), w.numel()))
+            host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+            seg = torch.empty_like(host, device=self.dev).copy_(host, non_blocking=True)
+            inv = torch.ones(len(ws), device=self.dev)
+            amax_ws = torch.zeros(len(ws), dtype=torch.int32, device=self.dev)
+            self._seg = (key, seg, amax_ws, inv, host)
+        _, seg, amax_ws, inv, _ = self._seg
+        ops.fp8_quantize_segments(seg, amax_ws, inv)
+        self._w = {n: (self._wbuf[n], inv[k:k + 1]) for k, (n, _) in enumerate(ws)}
+        self._wkey = self.eng._wgen
 
     def site(self, name):
         i = self.sites.get(name)

@@ -292,6 +292,16 @@ def fp8_quantize(x, q, inv_scale, workspace=None):
     return q
 
 
+def fp8_quantize_segments(seg, amax_ws, inv, blocks_per_seg=64):
+    """Batched fp8_quantize: seg int64 [nseg, 3] on the device = (src bf16
+    ptr, dst uint8 ptr, n); inv fp32 [nseg] <- amax / 448 per tensor."""
+    n = seg.shape[0]
+    if amax_ws.numel() < n or inv.numel() < n:
+        raise ValueError("fp8_quantize_segments: workspace / inv smaller than nseg")
+    call("smer_fp8_quantize_segments", n, _p(seg), _p(amax_ws), _p(inv), int(blocks_per_seg),
+         _stream())
+
+
 def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
              seed=0):
     """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ epilogue).  Returns False

@@ -1,5 +1,7 @@
+# C4 train step kernel statistics, fp8 and bf16 (rocprofv3 --kernel-trace --stats)
 set -e
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-infill --no-cpu --no-roofline > gpurun_out/b_c4.log 2>&1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4 -o run -- python3 tools/c4_step.py fp8 > gpurun_out/prof_c4.log 2>&1
+for p in fp8 bf16; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4_$p -o run -- python3 tools/c4_step.py $p 4 > gpurun_out/prof_c4_$p.log 2>&1
+done

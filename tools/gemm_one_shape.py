@@ -1,5 +1,5 @@
 """Run one GEMM shape N times (for rocprofv3 counter passes).
-    python tools/gemm_one_shape.py fwd|dgrad|wgrad M N K [iters]"""
+    python tools/gemm_one_shape.py fwd|fp8|dgrad|wgrad M N K [iters]"""
 import os
 import sys
 
@@ -16,6 +16,17 @@ if kind == "fwd":
     w = torch.randn(N, K, device="cuda").to(bf)
     b = torch.randn(N, device="cuda")
     f = lambda: ops.linear(x, w, b)  # noqa: E731
+elif kind == "fp8":
+    x = torch.randn(M, K, device="cuda").to(bf)
+    w = torch.randn(N, K, device="cuda").to(bf)
+    b = torch.randn(N, device="cuda")
+    x8 = torch.empty(M, K, device="cuda", dtype=torch.uint8)
+    w8 = torch.empty(N, K, device="cuda", dtype=torch.uint8)
+    xi, wi = torch.empty(1, device="cuda"), torch.empty(1, device="cuda")
+    ops.fp8_quantize(x, x8, xi)
+    ops.fp8_quantize(w, w8, wi)
+    out = torch.empty(M, N, device="cuda", dtype=bf)
+    f = lambda: ops.gemm_fp8(x8, xi, w8, wi, out, bias=b)  # noqa: E731
 elif kind == "dgrad":
     dy = torch.randn(M, K, device="cuda").to(bf)
     w = torch.randn(K, N, device="cuda").to(bf)
