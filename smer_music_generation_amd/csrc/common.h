@@ -240,6 +240,27 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // and folds max|v| into this step's amax.  Consumers dequantise with
 // inv = 1 / qs.  amax is kept as float bits (non-negative floats order like
 // unsigned ints, so integer atomicMax is exact and arrival-order free).
+//
+// v_cvt_pk_fp8_f32 is exact nearest-even on any f32 (tools/probes/
+// cvt_fp8_probe.hip: 1.08 M values around every e4m3 midpoint, 0 mismatches
+// against a software nearest-even), so the cast is the whole rounding.
+// Workgroup barrier that settles only LDS traffic (lgkmcnt(0), vmcnt /
+// expcnt left at their maxima): GEMM epilogue passes reuse an LDS staging
+// tile, so the next pass needs the LDS writes / reads of the last one done,
+// not its global stores (__syncthreads waits vmcnt(0): every pass would pay
+// the store round trip).  The asm memory clobbers keep the compiler from
+// moving memory operations across it.
+__device__ __forceinline__ void smer_lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Correctly rounded f32 quotient for the scales (448 / amax and back): via
+// f64 the double rounding is exact for a quotient of f32 operands, whatever
+// the f32 '/' lowering; the scale enters every product before the cast.
+__device__ __forceinline__ float smer_div_rn(float a, float b) { return (float)((double)a / (double)b); }
 __device__ __forceinline__ uint2 smer_q8x8(const float (&v)[8], float qs) {
   uint32_t w[2];
 #pragma unroll

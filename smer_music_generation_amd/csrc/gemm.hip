@@ -643,7 +643,10 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
             ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
       }
     }
-    __syncthreads();  // ep rows written; X(pass) landed; X(pass-1) slot free
+    // ep rows written; X(pass) landed; X(pass-1) slot free (the residual /
+    // gate DMA needs vmcnt; without one only LDS traffic must settle)
+    if (xsrc) __syncthreads();
+    else smer_lds_barrier();
     if (xsrc && pass >= 1 && pass < 3)
       g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
     const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
@@ -685,7 +688,8 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
         amax_acc = fmaxf(amax_acc, smer_absmax8(v));
       }
     }
-    __syncthreads();
+    if (xsrc) __syncthreads();
+    else smer_lds_barrier();
   }
 }
 
@@ -789,7 +793,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
               ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
         }
       }
-      __syncthreads();
+      smer_lds_barrier();  // LDS settled; stores left in flight
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
@@ -803,7 +807,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
           epi_apply8(e, M, N, grow, gcol, v);
         }
       }
-      __syncthreads();
+      smer_lds_barrier();  // LDS settled; stores left in flight
     }
   }
 }
@@ -1477,7 +1481,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
               ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
         }
       }
-      __syncthreads();  // (pass 0: also the bias slice)
+      smer_lds_barrier();  // (pass 0: also the bias slice); stores left in flight
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
@@ -1489,7 +1493,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
         epi_apply8(eb, M, N, grow, gcol, v, &amax_acc);
       }
-      __syncthreads();
+      smer_lds_barrier();
     }
   }
   if (Q8) smer_amax_commit(e.q8_amax, amax_acc);
@@ -1525,8 +1529,8 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(int rows, int cols, cons
                                                        const unsigned int* __restrict__ amax,
                                                        float* __restrict__ inv) {
   const float am = __uint_as_float(*amax);
-  const float sc = am > 0.f ? 448.f / am : 1.f;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *inv = 1.f / sc;
+  const float sc = am > 0.f ? smer_div_rn(448.f, am) : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *inv = smer_div_rn(1.f, sc);
   const int cpr = cols >> 3;
   const long n = (long)rows * cpr;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -1578,8 +1582,8 @@ __global__ __launch_bounds__(256) void quant_seg_kernel(const int64_t* __restric
   uint8_t* q = reinterpret_cast<uint8_t*>(seg[3 * s + 1]);
   const long n8 = seg[3 * s + 2] >> 3;
   const float am = __uint_as_float(amax[s]);
-  const float sc = am > 0.f ? 448.f / am : 1.f;
-  if (blockIdx.x == 0 && threadIdx.x == 0) inv[s] = 1.f / sc;
+  const float sc = am > 0.f ? smer_div_rn(448.f, am) : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) inv[s] = smer_div_rn(1.f, sc);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + 8 * i);
     float f[8];

@@ -358,8 +358,8 @@ __global__ void fp8_scales_kernel(int n, const unsigned* __restrict__ amax_prev,
   if (i >= n) return;
   const float a = __uint_as_float(amax_prev[i]);
   const bool ok = a > 0.f && a < 3.0e38f;
-  qs[i] = ok ? 448.f / a : 1.f;
-  inv[i] = ok ? a / 448.f : 1.f;
+  qs[i] = ok ? smer_div_rn(448.f, a) : 1.f;
+  inv[i] = ok ? smer_div_rn(a, 448.f) : 1.f;
   amax_next[i] = 0u;
 }
 

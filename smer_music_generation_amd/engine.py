@@ -40,6 +40,14 @@ class _W:
     pass
 
 
+# fp8 mode: FFN1 also writes the e4m3 copy of its ReLU output so that FFN2
+# runs on the fp8 MFMA too.  Measured at C4 (profiles/r02_c4_fp8_gemm.txt):
+# that extra 1-byte stream costs the FFN1 epilogue more (+76 us, 65536 x
+# 2048) than FFN2 gains over bf16 (-10 us: residual-bound epilogue), so by
+# default FFN1 runs fp8 with a bf16 output only and FFN2 stays bf16.
+FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "0") == "1"
+
+
 class Engine:
     def __init__(self, model):
         self.m = model
@@ -241,9 +249,12 @@ class Engine:
     def _lin(self, f8, x, xq, wname, w, b, q_site=None, **epi):
         """x @ w^T + epilogue: on the fp8 MFMA when x has an e4m3 copy xq and
         the shape tiles, else bf16.  q_site: also write the e4m3 copy of the
-        output (returns (out, (q, site)))."""
+        output (returns (out, (q, site)) — (out, None) when the FFN2 input
+        copy is disabled, see FP8_FFN2)."""
         M, K = x.shape
         N = w.shape[0]
+        if q_site is not None and not FP8_FFN2:
+            return self._lin(f8, x, xq, wname, w, b, **epi), None
         if f8 is not None and xq is not None:
             from .fp8 import eligible
             if eligible(M, N, K) and epi.get("gate") is None:

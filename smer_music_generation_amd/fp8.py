@@ -2,12 +2,13 @@
 
 BASELINE.json configs[3] (C4) asks for fp8 MFMA GEMMs on CDNA4.  In the
 `precision="fp8"` mode the forward contractions whose input comes from a
-LayerNorm or from the FFN1 epilogue run on the block-scaled fp8 MFMA
-(`smer_gemm_fp8`): the QKV in-projections of layers >= 1, FFN1, FFN2, the
-decoder's cross-attention Q and the stacked cross-attention K/V of the memory
-(`transformer.py:389,393,459,463,467`).  Out-projections (input: attention
-output), the vocab head and every backward GEMM stay bf16; master weights fp32,
-working weights bf16.
+LayerNorm run on the block-scaled fp8 MFMA (`smer_gemm_fp8`): the QKV
+in-projections of layers >= 1, FFN1, the decoder's cross-attention Q and the
+stacked cross-attention K/V of the memory (`transformer.py:389,393,459,463,
+467`); FFN2 too when FFN1 writes an e4m3 copy of its output
+(engine.FP8_FFN2, off by default: measured slower at C4).  Out-projections
+(input: attention output), the vocab head and every backward GEMM stay bf16;
+master weights fp32, working weights bf16.
 
 Scaling (no standalone quantise pass over activations):
   * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy

@@ -591,6 +591,14 @@ def test_linear_decode_kv_scatter(M, N, K):
 
 
 # ------------------------------------------------------------ fp8
+def _e4m3_ref(x, amax):
+    """e4m3 bytes of x * (448 / amax): f32 scale by IEEE division, f32
+    product, clamp, torch's CPU float8_e4m3fn cast (nearest-even)."""
+    sc = np.float32(448.0) / np.float32(amax)
+    y = x.float().cpu().numpy().astype(np.float32) * sc
+    return torch.from_numpy(np.clip(y, -448, 448)).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
 def test_gemm_fp8_exact_integer_layout():
     """fp8 MFMA fragment / output layout with exact small-integer e4m3 data
     and an asymmetric B: the kernel must reproduce A.B^T exactly."""
@@ -627,17 +635,11 @@ def test_fp8_quantize_and_gemm():
     torch.cuda.synchronize()
     amax = x.float().abs().max()
     assert abs(xi.item() - amax.item() / 448) < 1e-6 * amax.item()
-    # reference cast on the CPU (torch's CPU float8 conversion: RNE, saturated by the clamp)
-    xc = x.float().cpu()
-    ref8 = (xc * (448 / amax.cpu())).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
-    got8 = x8.cpu()
-    bad = (ref8 != got8)
-    if bad.any():
-        for i, j in bad.nonzero()[:6].tolist():
-            print("mismatch x=%r scaled=%r ref=%d got=%d" % (xc[i, j].item(), (xc[i, j] * (448 / amax.cpu())).item(),
-                                                             ref8[i, j].item(), got8[i, j].item()))
-    agree = 1.0 - bad.float().mean().item()
-    assert agree > 0.999, agree
+    # reference: the f32 scale by IEEE division (torch's `448 / t` is a
+    # reciprocal times 448, 1 ulp off at times), the f32 product, torch's CPU
+    # e4m3 cast (nearest-even) of the clamped value
+    ref8 = _e4m3_ref(x, amax.item())
+    assert torch.equal(x8.cpu(), ref8)
     bias = torch.randn(N, device=dev)
     res = torch.randn(M, N, device=dev).to(torch.bfloat16)
     C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -647,6 +649,24 @@ def test_fp8_quantize_and_gemm():
     err = ((C.float() - ref).norm() / ref.norm()).item()
     assert err < 0.05, err
     assert not O.gemm_fp8(x8[:100], xi, w8, wi, C[:100])  # outside the tiling: caller falls back
+
+
+def test_fp8_quantize_rounds_nearest_even_near_midpoints():
+    """amax = 15.75 puts x * (448 / amax) on or next to e4m3 midpoints for
+    many bf16 x (1.4765625 * 28.444445 = 42.0 exactly, a tie -> 40; with the
+    1-ulp-high scale torch's `448 / t` gives, 42.0000038 -> 44): the scale
+    must be the correctly rounded quotient and the cast nearest-even."""
+    O = ops()
+    M, K = 256, 512
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = (torch.randn(M, K, generator=g) * 3).clamp(-15.0, 15.0).to(torch.bfloat16)
+    x[0, 0] = 15.75
+    xd = x.to(dev)
+    x8 = torch.empty(M, K, device=dev, dtype=torch.uint8)
+    xi = torch.empty(1, device=dev)
+    O.fp8_quantize(xd, x8, xi)
+    torch.cuda.synchronize()
+    assert torch.equal(x8.cpu(), _e4m3_ref(x, 15.75))
 
 
 def test_fp8_quantize_segments_matches_per_tensor():
