@@ -24,6 +24,7 @@
  *   smer_kv_scatter      append new K/V rows to a per-request cache
  *   smer_kv_scatter_heads  the cross-attention memory K/V (transformer.py:463)
  *                        into a head-major per-request cache at prefill
+ *   smer_linear_decode_ln  the same with the LayerNorm of its input fused in
  *   smer_linear_decode   decode-step Linear (M <= 256 rows) whose epilogue
  *                        also appends the new K/V columns to the cache
  *                        (transformer.py:459 per generated token)
@@ -165,6 +166,16 @@ int smer_linear_decode(int M, int N, int K, const void* A, long lda, const void*
                        long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
                        long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
                        int kv_col0, smer_stream_t stream);
+/* smer_linear_decode with the post-norm LayerNorm in its prologue: the
+ * Linear's input is LN(Y) (row statistics and normalisation bit-identical
+ * to smer_layernorm_fwd with the same eps), also stored to X when X is
+ * given (the residual of the next sublayer).  K % 8 == 0, K <= 2048. */
+int smer_linear_decode_ln(int M, int N, int K, const void* Y, long ldy, const float* gamma,
+                          const float* beta, float eps, void* X, long ldx, const void* W, long ldw,
+                          const float* bias, int relu, const void* residual, long ldr, void* C,
+                          long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
+                          long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
+                          int kv_col0, smer_stream_t stream);
 /* One greedy grammar step for R requests (generation.py:528-687).
  * logits: fp32 [2R, >=V] rows (request r's last fed token at row 2r+1).
  * state: int32 [R, nst>=9] = pos, flags(sep|cont<<1|pitch<<2|rest<<3), span

@@ -44,6 +44,9 @@ SIGNATURES = {
     "smer_kv_scatter": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, c_long, P, P, P]),
     "smer_linear_decode": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
                                    P, c_long, P, c_long, P, c_long, c_long, P, P, c_int, P]),
+    "smer_linear_decode_ln": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
+                                      c_long, P, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
+                                      c_long, P, P, c_int, P]),
     "smer_fp8_quantize_workspace": (c_size, []),
     "smer_fp8_quantize": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P]),
     "smer_fp8_quantize_segments": (c_int, [c_int, P, P, P, c_int, P]),

@@ -1297,6 +1297,150 @@ extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* 
   return SMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Decode Linear with the post-norm LayerNorm in its prologue (decode steps:
+// every LayerNorm of the decoder layer feeds a Linear, transformer.py:462,
+// 466,469 -> 459/463/389 of the next sublayer).  A workgroup owns 16 rows x
+// 16 output columns like the skinny kernel; it first normalises its 16 rows
+// (one wave per row: ln_row_stats / ln_apply, the very arithmetic of
+// ln_fwd_kernel, so the bits are the standalone LayerNorm's) into LDS —
+// the workgroups of column strip 0 also store them (the residual the next
+// sublayer adds) — then runs the K loop from LDS.  Saves the LayerNorm
+// launch and its HBM round trip per norm (3 of the ~11 launches per layer).
+// ---------------------------------------------------------------------------
+template <int NW, int UNR>
+__global__ __launch_bounds__(64 * NW) void gemm_skinny_ln_kernel(int M, int N, int K,
+                                                                 const bf16* __restrict__ Y, long ldy,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float eps,
+                                                                 bf16* __restrict__ X, long ldx,
+                                                                 const bf16* __restrict__ B, long ldb,
+                                                                 GemmEpi e) {
+  constexpr int BM = 16;
+  extern __shared__ __attribute__((aligned(16))) char xs[];  // BM rows x (2K + 32) bytes
+  __shared__ float red[NW][BM][SK_BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * SK_BN, m0 = blockIdx.y * BM;
+  const long xs_ld = 2L * K + 32;  // +32 B: fragment reads of 16 rows hit 16 distinct bank quads
+  const int erow = m0 + (tid >> 1), ecol = n0 + (tid & 1) * 8;
+  const bool eth = tid < BM * 2;
+  const bool pre = eth && epi_pre_ok(e, M, N, erow, ecol);
+  EpiPre ep;
+  if (pre) epi_prefetch(e, erow, ecol, ep);
+  // the weight fragments of the first K round are requested before the
+  // LayerNorm prologue, so their HBM latency overlaps it (else two
+  // dependent round trips: rows, then weights)
+  const int r16 = lane & 15, kq = (lane >> 4) * 8;
+  const int ncol = n0 + r16;
+  const bool colok = ncol < N;
+  const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
+  const int nsteps = (K + 31) / 32;
+  bf16x8 b0[UNR];
+#pragma unroll
+  for (int u = 0; u < UNR; ++u) {
+    const int k = (wave + u * NW) * 32;
+    b0[u] = (colok && k + kq < K) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+  }
+  const int nch = K >> 3;
+  for (int rr = wave; rr < BM; rr += NW) {  // wave-uniform
+    const int row = m0 + rr;
+    char* dst = xs + rr * xs_ld;
+    if (row < M) {
+      float v[LNR_MAXC][8], mu, rs;
+      ln_row_stats<bf16>(Y + (long)row * ldy, K, eps, lane, v, mu, rs);
+#pragma unroll
+      for (int c = 0; c < LNR_MAXC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ch < nch) {
+          const float4 g0 = *reinterpret_cast<const float4*>(gamma + ch * 8);
+          const float4 g1 = *reinterpret_cast<const float4*>(gamma + ch * 8 + 4);
+          const float4 b0 = *reinterpret_cast<const float4*>(beta + ch * 8);
+          const float4 b1 = *reinterpret_cast<const float4*>(beta + ch * 8 + 4);
+          const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+          const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          bf16x8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = (bf16)ln_apply(v[c][i], mu, rs, g[i], b[i]);
+          *reinterpret_cast<bf16x8*>(dst + ch * 16) = o;
+          if (X && blockIdx.x == 0) *reinterpret_cast<bf16x8*>(X + (long)row * ldx + ch * 8) = o;
+        }
+      }
+    } else {
+      for (int ch = lane; ch < nch; ch += 64) *reinterpret_cast<bf16x8*>(dst + ch * 16) = bf16x8{};
+    }
+  }
+  __syncthreads();
+  const char* ap = xs + r16 * xs_ld + kq * 2;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s0 = wave; s0 < nsteps; s0 += NW * UNR) {
+    bf16x8 a[UNR], b[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int k = (s0 + u * NW) * 32;
+      const bool kok = k + kq < K;
+      if (s0 == wave) b[u] = b0[u];
+      else b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+      a[u] = kok ? *reinterpret_cast<const bf16x8*>(ap + 2 * k) : bf16x8{};
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) acc = mfma16(a[u], b[u], acc);
+  }
+  const int g = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][4 * g + r][r16] = acc[r];
+  __syncthreads();
+  if (eth) {
+    const int row = tid >> 1, ch = tid & 1;
+    if (erow < M && ecol < N) {
+      float v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[w][row][ch * 8 + c];
+        v[c] = t;
+      }
+      if (pre) epi_apply8_pre(e, erow, ecol, v, ep);
+      else epi_apply8(e, M, N, erow, ecol, v);
+    }
+  }
+}
+
+extern "C" int smer_linear_decode_ln(int M, int N, int K, const void* Y, long ldy, const float* gamma,
+                                     const float* beta, float eps, void* X, long ldx, const void* W,
+                                     long ldw, const float* bias, int relu, const void* residual,
+                                     long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
+                                     long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
+                                     const int32_t* kv_pos, int kv_col0, smer_stream_t stream) {
+  SMER_REQUIRE(M > 0 && M <= 4 * SK_BM && N > 0 && K > 0, "smer_linear_decode_ln: sizes (M <= 256)");
+  SMER_REQUIRE(K % 8 == 0 && K <= 64 * 8 * LNR_MAXC, "smer_linear_decode_ln: K % 8 == 0 and K <= 2048");
+  SMER_REQUIRE(Y && W && gamma && beta && (C || Cf), "smer_linear_decode_ln: null operand");
+  SMER_REQUIRE(ldy % 8 == 0 && ldw % 8 == 0 && aligned16(Y) && aligned16(W) && aligned16(gamma) &&
+                   aligned16(beta) && (!X || (aligned16(X) && ldx % 8 == 0)),
+               "smer_linear_decode_ln: strides / alignment");
+  SMER_REQUIRE(!kv || (kv_req && kv_pos && kv_col0 % 8 == 0 && kv_col0 >= 0 && kv_col0 < N &&
+                       aligned16(kv) && kv_row_stride % 8 == 0 && kv_req_stride % 8 == 0),
+               "smer_linear_decode_ln: kv scatter arguments");
+  GemmEpi e{};
+  e.bias = bias; e.alpha = 1.f; e.relu = relu; e.residual = residual; e.ldr = ldr;
+  e.drop_scale = 1.f; e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf;
+  e.kv = kv; e.kv_row_stride = kv_row_stride; e.kv_req_stride = kv_req_stride;
+  e.kv_req = kv_req; e.kv_pos = kv_pos; e.kv_col0 = kv_col0;
+  auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
+  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc) && a16(Cf, ldcf);
+  const dim3 grid((N + SK_BN - 1) / SK_BN, (M + 15) / 16);
+  const size_t lds = 16 * (2 * (size_t)K + 32);
+  hipStream_t s = (hipStream_t)stream;
+  if ((K + 31) / 32 > 16)
+    hipLaunchKernelGGL((gemm_skinny_ln_kernel<8, 4>), grid, dim3(512), lds, s, M, N, K, (const bf16*)Y, ldy,
+                       gamma, beta, eps, (bf16*)X, ldx, (const bf16*)W, ldw, e);
+  else
+    hipLaunchKernelGGL((gemm_skinny_ln_kernel<8, 2>), grid, dim3(512), lds, s, M, N, K, (const bf16*)Y, ldy,
+                       gamma, beta, eps, (bf16*)X, ldx, (const bf16*)W, ldw, e);
+  SMER_CHECK_LAUNCH("smer_linear_decode_ln");
+  return SMER_OK;
+}
+
 extern "C" int smer_linear_decode(int M, int N, int K, const void* A, long lda, const void* W,
                                   long ldw, const float* bias, int relu, const void* residual,
                                   long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,

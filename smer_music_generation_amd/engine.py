@@ -165,7 +165,7 @@ class Engine:
         key = (dt, work.data_ptr(), self._wgen, self._version_key())
         if self.n_dec and (self._ckv_all is None or self._ckv_all[0] != key):
             n2 = 2 * d
-            if self._ckv_all is not None and self._ckv_all[1].dtype == dt and \
+            if os.environ.get("SMER_CKV_REUSE", "1") == "1" and self._ckv_all is not None and self._ckv_all[1].dtype == dt and \
                     self._ckv_all[1].device == work.device and self._ckv_all[1].shape[0] == self.n_dec * n2:
                 wall, ball = self._ckv_all[1], self._ckv_all[2]  # rewritten in place (stable pointers)
             else:

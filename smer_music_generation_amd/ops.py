@@ -280,6 +280,24 @@ def linear_decode(x, w, bias=None, *, relu=False, residual=None, out=None, out_f
     return out if out is not None else out_f32
 
 
+def linear_decode_ln(y, gamma, beta, w, bias=None, *, x_out=None, eps=1e-5, relu=False,
+                     residual=None, out=None, out_f32=None, kv=None, kv_req=None, kv_pos=None,
+                     kv_row_stride=0, kv_req_stride=0, kv_col0=0):
+    """linear_decode(LayerNorm(y), w, ...): the LayerNorm fused into the
+    Linear's prologue (bit-identical to ops.layernorm); x_out receives LN(y)."""
+    M, K = y.shape
+    N = w.shape[0]
+    if out is None and out_f32 is None:
+        out = torch.empty(M, N, device=y.device, dtype=y.dtype)
+    call("smer_linear_decode_ln", M, N, K, _p(y), _ld(y), _p(gamma), _p(beta), float(eps), _p(x_out),
+         _ld(x_out) if x_out is not None else 0, _p(w), _ld(w), _p(bias), int(bool(relu)),
+         _p(residual), _ld(residual) if residual is not None else 0, _p(out),
+         _ld(out) if out is not None else 0, _p(out_f32), _ld(out_f32) if out_f32 is not None else 0,
+         _p(kv), int(kv_row_stride), int(kv_req_stride), _p(kv_req), _p(kv_pos), int(kv_col0),
+         _stream())
+    return out if out is not None else out_f32
+
+
 # ---------------------------------------------------------------------------
 def fp8_quantize(x, q, inv_scale, workspace=None):
     """q (uint8 e4m3 bits, same shape as x) = e4m3(x * 448 / amax|x|);

@@ -590,6 +590,41 @@ def test_linear_decode_kv_scatter(M, N, K):
     assert torch.equal(cache[req.long(), pos.long()], out[:, col0:])
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 512, 512), (37, 309, 512), (128, 2048, 512), (16, 1536, 512),
+                                   (24, 512, 2048)])
+def test_linear_decode_ln_is_layernorm_then_linear(M, N, K):
+    """The LayerNorm-prologue decode Linear == ops.layernorm then
+    ops.linear_decode, bit for bit (stored LN output, GEMM output, K/V
+    append), incl. ragged M / N and the fp32 logits head."""
+    O = ops()
+    bf = torch.bfloat16
+    y = (torch.randn(M, K, device=dev) * 2 + 0.5).to(bf)
+    g = torch.randn(K, device=dev)
+    be = torch.randn(K, device=dev)
+    w = (torch.randn(N, K, device=dev) / math.sqrt(K)).to(bf)
+    b = torch.randn(N, device=dev)
+    xln = torch.empty_like(y)
+    O.layernorm(y, g, be, xln, torch.empty(M, device=dev), torch.empty(M, device=dev))
+    x_out = torch.empty_like(y)
+    col0 = (N // 3) // 8 * 8
+    wk = (N - col0 + 7) // 8 * 8  # cache row stride (multiple of 8)
+    R, T = 5, M // 5 + 1
+    c1 = torch.zeros(R, T, wk, device=dev, dtype=bf)
+    c2 = torch.zeros_like(c1)
+    req = torch.arange(M, device=dev, dtype=torch.int32) % R
+    pos = torch.arange(M, device=dev, dtype=torch.int32) // R
+    kv = dict(kv_req=req, kv_pos=pos, kv_row_stride=wk, kv_req_stride=T * wk, kv_col0=col0)
+    ref = O.linear_decode(xln, w, b, relu=True, kv=c1, **kv)
+    got = O.linear_decode_ln(y, g, be, w, b, relu=True, x_out=x_out, kv=c2, **kv)
+    lf_ref = O.linear_decode(xln, w, b, out_f32=torch.empty(M, N, device=dev))
+    lf_got = O.linear_decode_ln(y, g, be, w, b, out_f32=torch.empty(M, N, device=dev))
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, xln)
+    assert torch.equal(got, ref)
+    assert torch.equal(c2, c1)
+    assert torch.equal(lf_got, lf_ref)
+
+
 # ------------------------------------------------------------ fp8
 def _e4m3_ref(x, amax):
     """e4m3 bytes of x * (448 / amax): f32 scale by IEEE division, f32
