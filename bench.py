@@ -392,6 +392,23 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
+def data_feed(per_gpu_tokens_per_s, seconds=3.0):
+    """Host side of the training input: one process's rate of
+    the pretraining pipeline (stack_batches groups -> span masking -> collate,
+    control mode 2) in the trainer's unit, and the worker processes one GPU
+    needs at the measured train rate."""
+    import math as _m
+    from smer_music_generation_amd.data import measure_rate
+    r = measure_rate(seconds, 2, True)
+    f = measure_rate(seconds / 2, 2, False)
+    need = per_gpu_tokens_per_s / r["tokens_per_s"]
+    return {"metric": "pretraining items + collate, collated B*(S+T) tokens/s per host process",
+            "value": round(r["tokens_per_s"], 1), "finetune_value": round(f["tokens_per_s"], 1),
+            "ids_per_s": round(r["ids_per_s"], 1), "processes_per_gpu": _m.ceil(need),
+            "train_tokens_per_s_per_gpu": round(per_gpu_tokens_per_s, 1),
+            "source": "synthetic corpus (240 songs, 8-24 bars), max_token_length 2200"}
+
+
 def main():
     args = parse_args()
 
@@ -429,6 +446,7 @@ def main():
             dist.all_reduce(sec, op=dist.ReduceOp.MAX)
             c5["tokens_per_s"] = t.item() / sec.item()
     cpu = cpu_baseline(args) if (args.cpu and rank == 0 and world == 1) else None
+    feed = data_feed(tr["tokens_per_s"] / world) if (args.cpu and rank == 0) else None
 
     if rank == 0:
         roof = None
@@ -494,6 +512,7 @@ def main():
                                  "roofline": c5["roofline"],
                                  "phases_s": c5["phases_s"], "parallelism": "replicas"},
             "cpu_baseline": cpu,
+            "data_pipeline": feed,
         }
         print(json.dumps(line))
     if world > 1:

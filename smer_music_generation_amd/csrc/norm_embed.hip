@@ -95,7 +95,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
   }
 }
 
-constexpr int LN_BWD_ROWS = 64;  // rows per workgroup (16 per wave)
+// rows per workgroup: 64 (16 per wave) for large M; 16 (one RB batch of 4
+// per wave) when 64 would leave the grid under ~2 workgroups per CU (the
+// decoder's 8192 rows: 19.6 vs 23.9 us; 64 stays better at 32768 rows,
+// where 4x the column partials cost more than the extra parallelism gives)
+constexpr int LN_BWD_ROWS = 64;
+constexpr int LN_BWD_ROWS_SMALL = 16;
+static inline int ln_bwd_rows(int M) { return M <= 16384 ? LN_BWD_ROWS_SMALL : LN_BWD_ROWS; }
 
 // One wave per row, NC 16-B chunks per lane (N <= 512 * NC); a wave takes
 // its 16 rows of the block RB at a time with all RB rows' loads issued
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
                                                      T* __restrict__ dx, long lddx,
                                                      T* __restrict__ dxd, long ldxd,
                                                      uint32_t thr, uint32_t seed, float dscale,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, int rows_per_blk) {
   constexpr int LN_MAXC = NC;
   __shared__ float red[4][2][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -124,8 +130,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
 #pragma unroll
     for (int i = 0; i < 8; ++i) { pg[c][i] = 0.f; pb[c][i] = 0.f; }
   }
-  const int r0 = blockIdx.x * LN_BWD_ROWS;
-  for (int rb = 0; rb < LN_BWD_ROWS / 4; rb += RB) {
+  const int r0 = blockIdx.x * rows_per_blk;
+  for (int rb = 0; rb < rows_per_blk / 4; rb += RB) {
     float xh[RB][NC][8], gd[RB][NC][8], mu[RB], rs[RB];
     bool ok[RB];
 #pragma unroll
@@ -374,7 +380,7 @@ extern "C" int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, floa
 }
 
 extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
-  size_t nblk = (size_t)(M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  size_t nblk = (size_t)(M + ln_bwd_rows(M) - 1) / ln_bwd_rows(M);
   return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, 2 * N);
 }
 
@@ -391,7 +397,8 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
                "smer_layernorm_bwd: workspace too small");
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  int nblk = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  const int rpb = ln_bwd_rows(M);
+  int nblk = (M + rpb - 1) / rpb;
   uint32_t thr = smer_drop_thr16(drop_p);
   float ds = smer_drop_scale16(thr);
   float* part = params ? (float*)workspace : nullptr;
@@ -399,7 +406,7 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
 #define LNB1(T, F, NC, RB)                                                                     \
   hipLaunchKernelGGL((ln_bwd_kernel<T, F, NC, RB>), dim3(nblk), dim3(256), 0, s, M, N, dy,     \
                      lddy, (const T*)x, ldx, mean, rstd, gamma, (T*)dx, lddx, (T*)dx_drop, ldxd, \
-                     thr, seed, ds, part)
+                     thr, seed, ds, part, rpb)
 #define LNB(T, F)                                  \
   do {                                             \
     if (N <= 512) LNB1(T, F, 1, 4);                \
