@@ -70,6 +70,16 @@ def test_abi_library_exports_every_header_symbol():
     assert lib.smer_abi_version() == 1
 
 
+def test_data_library_exports_every_header_symbol():
+    import ctypes
+    hdr = open(os.path.join(ROOT, "include", "smer_data.h")).read()
+    decl = set(re.findall(r"\b(smer_[a-z0-9_]+)\(", hdr))
+    assert decl == {"smer_span_mask", "smer_mt_random"}
+    lib = ctypes.CDLL(os.path.join(ROOT, "smer_music_generation_amd", "libsmer_data.so"))
+    for name in decl:
+        assert hasattr(lib, name), name
+
+
 def test_ops_reject_cpu_tensors():
     from smer_music_generation_amd import ops
     x = torch.zeros(4, 8)

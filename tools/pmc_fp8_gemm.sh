@@ -1,5 +1,7 @@
 #!/bin/bash
-# fp8 vs bf16 forward GEMM counters (one shape): MFMA busy, clocks, waits.
+# fp8 vs bf16 forward GEMM counters (one shape, M65536 N2304 K3072): MFMA busy,
+# LDS bank conflicts, waits (tools/pmc_sq.py), kernel durations.
+# Usage (GPU box, repo root): bash tools/pmc_fp8_gemm.sh
 set -e
 export TMPDIR=/tmp
 R=$PWD

@@ -1,4 +1,5 @@
 # C4 train step kernel statistics, fp8 and bf16 (rocprofv3 --kernel-trace --stats)
+# Usage (GPU box, repo root): bash tools/prof_c4.sh
 set -e
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Profile the headline bench: kernel-trace stats + separate PMC passes for
 # FETCH_SIZE and WRITE_SIZE (never combined with other tracing domains),
-# plus the decode step (graph replays).
+# plus the decode step (graph replays), its HBM bytes (separate PMC passes),
+# the C4 fp8 / bf16 train steps, SQ counters of the train step and of the
+# fp8 vs bf16 forward GEMM.
 # Usage (on the GPU box, from the repo root): bash tools/profile_round.sh <tag>
 set -e
 export TMPDIR=/tmp
@@ -23,4 +25,14 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/d
 # the product path (weight-gradient stream overlap on), timed steps only
 SMER_WGRAD_OVERLAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_ovl -o run -- \
   python3 $R/bench.py --steps 5 --warmup 2 --no-infill --no-cpu --no-c4 --no-roofline > $OUT/trace_ovl.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/dec_fetch -o run -- \
+  python3 $R/tools/prof_decode.py --n 20 --graph > $OUT/dec_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/dec_write -o run -- \
+  python3 $R/tools/prof_decode.py --n 20 --graph > $OUT/dec_write.log 2>&1
+for p in fp8 bf16; do
+  SMER_WGRAD_OVERLAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4_$p -o run -- \
+    python3 $R/tools/c4_step.py $p 4 > $OUT/c4_$p.log 2>&1
+done
+bash $R/tools/profile_pmc.sh $TAG > $OUT/pmc_sq.log 2>&1
+bash $R/tools/pmc_fp8_gemm.sh > $OUT/pmc_fp8.log 2>&1
 echo done

@@ -1,7 +1,7 @@
 """Write the committed profile summaries under profiles/ from a
 tools/profile_round.sh run (gpurun_out/prof_<tag>/).
 
-    python tools/refresh_profiles.py r01 [train_steps_traced]
+    python tools/refresh_profiles.py r02 [train_steps_traced]
 """
 import json
 import os
@@ -63,4 +63,35 @@ with open(os.path.join(dst, tag + "_train_pmc_traffic.txt"), "w") as f:
     f.write("# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 2 "
             "--warmup 1 --no-infill --no-cpu --no-roofline --no-c4; FETCH doubled per gfx950 "
             "correction (MI355X_MICROARCH.md HBM)\n" + txt)
+# decode HBM bytes per kernel (separate FETCH / WRITE passes over 20 graph replays)
+dfetch = os.path.join(src, "dec_fetch", "run_counter_collection.csv")
+dwrite = os.path.join(src, "dec_write", "run_counter_collection.csv")
+if os.path.exists(dfetch) and os.path.exists(dwrite):
+    with open(os.path.join(dst, tag + "_decode_pmc_traffic.json"), "w") as f:
+        json.dump({k[5:] if k.startswith("void ") else k: v for k, v in summary(dfetch, dwrite).items()},
+                  f, indent=1)
+    txt = run(os.path.join(ROOT, "tools", "pmc_traffic.py"), dfetch, dwrite)
+    with open(os.path.join(dst, tag + "_decode_pmc_traffic.txt"), "w") as f:
+        f.write("# rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/prof_decode.py "
+                "--n 20 --graph (R=32, S=1000, incl. prefill); FETCH doubled per gfx950 correction\n" + txt)
+
+# C4 train step, fp8 and bf16 (product path, 5 steps traced: 1 warm-up + 4)
+for p in ("fp8", "bf16"):
+    c = os.path.join(src, "c4_" + p, "run_kernel_stats.csv")
+    if os.path.exists(c):
+        t = run(os.path.join(ROOT, "tools", "prof_summary.py"), c, "5", "30")
+        with open(os.path.join(dst, "%s_c4_%s_kernel_stats.txt" % (tag, p)), "w") as f:
+            f.write("# rocprofv3 --kernel-trace --stats -- python3 tools/c4_step.py %s 4 (C4: 12+12 "
+                    "layers d768 h12 S2048 T512 B32; weight gradients on the side stream; 5 steps "
+                    "traced; per-step = total/5)\n" % p + t)
+
+# SQ counters (train step, weight gradients serialised) and the fp8 GEMM pair
+for name, sub in (("train_pmc_sq", os.path.join("..", "pmc_" + tag, "sq.txt")),
+                  ("fp8_gemm_pmc_sq", os.path.join("..", "pmc_fp8", "sq.txt"))):
+    fsq = os.path.normpath(os.path.join(src, sub))
+    if os.path.exists(fsq):
+        shutil.copy(fsq, os.path.join(dst, "%s_%s.txt" % (tag, name)))
+        js = fsq[:-4] + ".json"
+        if os.path.exists(js):
+            shutil.copy(js, os.path.join(dst, "%s_%s.json" % (tag, name)))
 print(train.splitlines()[-2:], dec.splitlines()[-2:])
