@@ -25,6 +25,7 @@
  *   smer_kv_scatter_heads  the cross-attention memory K/V (transformer.py:463)
  *                        into a head-major per-request cache at prefill
  *   smer_linear_decode_ln  the same with the LayerNorm of its input fused in
+ *   smer_attn_decode_qln  decode cross attention with LN + query projection fused in
  *   smer_linear_decode   decode-step Linear (M <= 256 rows) whose epilogue
  *                        also appends the new K/V columns to the cache
  *                        (transformer.py:459 per generated token)
@@ -166,6 +167,18 @@ int smer_linear_decode(int M, int N, int K, const void* A, long lda, const void*
                        long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
                        long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
                        int kv_col0, smer_stream_t stream);
+/* Decode cross attention with its query projection and the LayerNorm in
+ * front of it fused in (transformer.py:462 -> 459 -> 463): the (head, row)
+ * block normalises the pre-norm row y (bits of smer_layernorm_fwd; stored
+ * to x_out by the head-0 blocks when given), forms q_h = bf16(LN(y) .
+ * wq[h*D..h*D+D-1]^T + bq[h*D..]) and attends like smer_attn_decode over
+ * the cache.  bf16, D == 64, dmodel in {512, 768, 1024}. */
+int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, long ldy, const float* gamma,
+                         const float* beta, float eps, const void* wq, long ldw, const float* bq,
+                         void* x_out, long ldx, int dmodel, const void* kcache, const void* vcache,
+                         long row_stride, long req_stride, long head_stride, const int32_t* row_req,
+                         const int32_t* row_nkeys, void* o, long ldo, float scale,
+                         smer_stream_t stream);
 /* smer_linear_decode with the post-norm LayerNorm in its prologue: the
  * Linear's input is LN(Y) (row statistics and normalisation bit-identical
  * to smer_layernorm_fwd with the same eps), also stored to X when X is

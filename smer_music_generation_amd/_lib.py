@@ -39,6 +39,9 @@ SIGNATURES = {
                                   P, P, c_int, c_float, P, P]),
     "smer_attn_decode": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, P, c_long, c_long,
                                  c_long, P, P, P, c_long, c_float, P]),
+    "smer_attn_decode_qln": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
+                                     P, c_long, c_int, P, P, c_long, c_long, c_long, P, P, P, c_long,
+                                     c_float, P]),
     "smer_kv_scatter_heads": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_long,
                                       c_long, P, P, P]),
     "smer_kv_scatter": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, c_long, P, P, P]),

@@ -1057,11 +1057,75 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-template <typename T, int LPK, int UNR, int NW, bool PIPE = false>
+// The cross-attention query projection with the LayerNorm in front of it
+// (transformer.py:462 -> 459 -> 463), computed inside the decode attention
+// block of (head h, row r): y is the pre-norm row, the block normalises it
+// (ln_row_stats / ln_apply: the LayerNorm kernel's bits; blocks of head 0
+// store it, the next sublayer's residual) and forms its head's D query
+// values as a bf16-rounded x . Wq_h^T + bq_h (fp32 dot products, 512 / D
+// threads per output), replacing the cross-Q Linear launch.
+struct DecQ {
+  const bf16* y;
+  long ldy;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const bf16* wq;  // [H*D rows, dmodel] (this head: rows h*D ..)
+  long ldw;
+  const float* bq;
+  bf16* x_out;
+  long ldx;
+  int dmodel;
+};
+
+template <int D, int NT, int DM>
+__device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int tid, float* qs,
+                                               bf16* xs) {
+  constexpr int TPO = NT / D;    // threads per query value
+  constexpr int KT = DM / TPO;   // K per thread (multiple of 8)
+  const int lane = tid & 63, wave = tid >> 6;
+  const int d = tid / TPO, part = tid % TPO;
+  // the head's weight row slice, requested before the row statistics
+  const bf16* wr = dq.wq + (long)(h * D + d) * dq.ldw + part * KT;
+  bf16x8 wv[KT / 8];
+#pragma unroll
+  for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+  if (wave == 0) {
+    float v[LNR_MAXC][8], mu, rs;
+    ln_row_stats<bf16>(dq.y + (long)r * dq.ldy, dq.dmodel, dq.eps, lane, v, mu, rs);
+#pragma unroll
+    for (int c = 0; c < LNR_MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < (dq.dmodel >> 3)) {
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          o[i] = (bf16)ln_apply(v[c][i], mu, rs, dq.gamma[ch * 8 + i], dq.beta[ch * 8 + i]);
+        *reinterpret_cast<bf16x8*>(xs + ch * 8) = o;
+        if (h == 0 && dq.x_out) *reinterpret_cast<bf16x8*>(dq.x_out + (long)r * dq.ldx + ch * 8) = o;
+      }
+    }
+  }
+  __syncthreads();
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < KT / 8; ++j) {
+    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + part * KT + 8 * j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc = fmaf((float)xv[i], (float)wv[j][i], acc);
+  }
+#pragma unroll
+  for (int w = 1; w < TPO; w <<= 1) acc += __shfl_xor(acc, w, 64);
+  if (part == 0) qs[d] = (float)(bf16)(acc + dq.bq[h * D + d]);
+  __syncthreads();
+}
+
+template <typename T, int LPK, int UNR, int NW, bool PIPE = false, int QP = 0>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
     long row_stride, long req_stride, long head_stride, const int32_t* __restrict__ row_req,
-    const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale) {
+    const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale,
+    DecQ dq = DecQ{}) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int GPW = 64 / LPK;  // key groups per wave
   constexpr int KPB = NW * GPW;  // keys per block step
@@ -1072,9 +1136,6 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   const int nk = row_nkeys[r];
   const long base = (long)row_req[r] * req_stride + h * head_stride + sub * VEC;
   float qv[VEC];
-  load16b<T>(q + (long)r * ldq + h * (LPK * VEC) + sub * VEC, qv);
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) qv[i] *= scale;
   float m = -INFINITY, l = 0.f, acc[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
@@ -1100,6 +1161,20 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   // before this step's math (two steps of K / V in flight per lane group;
   // measured 5.2 -> 5.7 TB/s at 4096 keys, slower at 1000)
   uint4 kr[UNR], vr[UNR];
+  if constexpr (QP > 0) {  // QP = d_model of the query prologue
+    static_assert(sizeof(T) == 2, "the query prologue is bf16");
+    __shared__ float qs[LPK * VEC];
+    __shared__ __attribute__((aligned(16))) bf16 xs[QP];
+    dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) qv[i] = qs[sub * VEC + i];
+  } else {
+    load16b<T>(q + (long)r * ldq + h * (LPK * VEC) + sub * VEC, qv);
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) qv[i] *= scale;
+  // (QP: requesting the first key step's K / V before the query prologue
+  // measured slower, 368 vs 336 us per decode step: issued after it)
   if (PIPE && nk > 0) load_step(0, kr, vr);
   for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
     uint4 kn[UNR], vn[UNR];
@@ -1431,6 +1506,51 @@ extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
   else
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_weights: dtype");
   SMER_CHECK_LAUNCH("smer_attn_weights");
+  return SMER_OK;
+}
+
+extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, long ldy,
+                                    const float* gamma, const float* beta, float eps, const void* wq,
+                                    long ldw, const float* bq, void* x_out, long ldx, int dmodel,
+                                    const void* kcache, const void* vcache, long row_stride,
+                                    long req_stride, long head_stride, const int32_t* row_req,
+                                    const int32_t* row_nkeys, void* o, long ldo, float scale,
+                                    smer_stream_t stream) {
+  SMER_REQUIRE(D == 64 && H > 0, "smer_attn_decode_qln: head dim 64");
+  SMER_REQUIRE(dmodel == 512 || dmodel == 768 || dmodel == 1024,
+               "smer_attn_decode_qln: d_model 512 / 768 / 1024 (else: Linear + smer_attn_decode)");
+  SMER_REQUIRE(y && gamma && beta && wq && bq && kcache && vcache && o && row_req && row_nkeys,
+               "smer_attn_decode_qln: null pointer");
+  auto al = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  SMER_REQUIRE(al(y) && al(wq) && al(kcache) && al(vcache) && al(o) && (!x_out || al(x_out)) &&
+                   ldy % 8 == 0 && ldw % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 && row_stride % 8 == 0 &&
+                   req_stride % 8 == 0 && head_stride % 8 == 0,
+               "smer_attn_decode_qln: 16-B alignment / strides");
+  if (n_rows == 0) return SMER_OK;
+  if (head_stride <= 0) head_stride = D;
+  DecQ dq{(const bf16*)y, ldy, gamma, beta, eps, (const bf16*)wq, ldw, bq, (bf16*)x_out, ldx, dmodel};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(H, n_rows);
+  // long memories (>= 2048 key rows of capacity): next key step's loads
+  // issued before the current step's math, as smer_attn_decode
+  const long cap_rows = head_stride != D ? head_stride / (row_stride > 0 ? row_stride : 1)
+                                         : req_stride / (row_stride > 0 ? row_stride : 1);
+  const bool pipe = cap_rows >= 2048;
+#define SMER_DEC_QLN(P, DM)                                                                        \
+  hipLaunchKernelGGL((attn_decode_vec_kernel<bf16, 8, 4, 8, P, DM>), grid, dim3(512), 0, s,        \
+                     (const bf16*)nullptr, 0L, (const bf16*)kcache, (const bf16*)vcache, row_stride, \
+                     req_stride, head_stride, row_req, row_nkeys, (bf16*)o, ldo, scale, dq)
+  if (pipe) {
+    if (dmodel == 512) SMER_DEC_QLN(true, 512);
+    else if (dmodel == 768) SMER_DEC_QLN(true, 768);
+    else SMER_DEC_QLN(true, 1024);
+  } else {
+    if (dmodel == 512) SMER_DEC_QLN(false, 512);
+    else if (dmodel == 768) SMER_DEC_QLN(false, 768);
+    else SMER_DEC_QLN(false, 1024);
+  }
+#undef SMER_DEC_QLN
+  SMER_CHECK_LAUNCH("smer_attn_decode_qln");
   return SMER_OK;
 }
 

@@ -24,6 +24,7 @@ replayed per token: one H2D of the row table, one replay, one D2H.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -168,11 +169,14 @@ class DecodeSession:
         """bf16 decoder step with every post-norm LayerNorm fused into the
         prologue of the Linear that consumes it (ops.linear_decode_ln: LN1 ->
         cross Q, LN2 -> FFN1, LN3 -> next layer's QKV, final norm -> vocab
-        head; the LN output is also stored as the next residual) and the new
-        K/V appended by the QKV epilogue: 8 launches per layer instead of 11."""
+        head; the LN output is also stored as the next residual), the cross
+        query projection computed inside the cross-attention blocks, and the
+        new K/V appended by the QKV epilogue: 7 launches per layer (11 in
+        round 1)."""
         eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
         H, D, M = eng.H, eng.D, self.M
         pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
+        self._qln = D == 64 and d in (512, 768, 1024) and os.environ.get("SMER_DECODE_QLN", "1") == "1"
         y_prev = n_prev = None
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
@@ -188,12 +192,18 @@ class DecodeSession:
                             row_stride=2 * d, req_stride=sstride, scale=scale)
             y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=x)
             x1 = torch.empty(M, d, dtype=dt, device=dev)
-            qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
             cc = self.cross_kv[li]
             oc = torch.empty(M, d, dtype=dt, device=dev)
-            ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
-                            row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
-                            scale=scale)
+            if self._qln:  # LN1 + cross Q inside the cross-attention blocks
+                ops.attn_decode_qln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, cc,
+                                    cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
+                                    row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
+                                    scale=scale, x_out=x1)
+            else:
+                qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
+                ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
+                                row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
+                                scale=scale)
             y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
             x2 = torch.empty(M, d, dtype=dt, device=dev)
             h = ops.linear_decode_ln(y2, L.n2[0], L.n2[1], L.l1_w, L.l1_b, relu=True, x_out=x2)

@@ -249,6 +249,17 @@ def attn_decode(q, kcache, vcache, row_req, row_nkeys, out, *, H, D, row_stride,
          _p(row_nkeys), _p(out), _ld(out), float(scale), _stream())
 
 
+def attn_decode_qln(y, gamma, beta, wq, bq, kcache, vcache, row_req, row_nkeys, out, *, H, D,
+                    row_stride, req_stride, scale, head_stride=0, x_out=None, eps=1e-5):
+    """Decode cross attention whose query is LayerNorm(y) . wq^T + bq, both
+    computed in the attention block (see smer_hip.h); x_out <- LayerNorm(y)."""
+    M, dm = y.shape
+    call("smer_attn_decode_qln", M, H, D, _p(y), _ld(y), _p(gamma), _p(beta), float(eps), _p(wq),
+         _ld(wq), _p(bq), _p(x_out), _ld(x_out) if x_out is not None else 0, dm, _p(kcache),
+         _p(vcache), int(row_stride), int(req_stride), int(head_stride), _p(row_req),
+         _p(row_nkeys), _p(out), _ld(out), float(scale), _stream())
+
+
 def kv_scatter_heads(src, cache, row_req, row_pos, *, H, D, req_stride, kv_stride, head_stride):
     """Rows of [K heads | V heads] into a head-major cache (see smer_hip.h)."""
     if src.shape[1] != 2 * H * D:

@@ -625,6 +625,38 @@ def test_linear_decode_ln_is_layernorm_then_linear(M, N, K):
     assert torch.equal(lf_got, lf_ref)
 
 
+@pytest.mark.parametrize("S,dm", [(300, 512), (2100, 512), (700, 768)])
+def test_attn_decode_qln_is_ln_linear_attention(S, dm):
+    """Decode cross attention with LN + query projection in its blocks ==
+    LayerNorm -> Linear -> smer_attn_decode: the stored LN output bit for bit,
+    the attention output within bf16 rounding of the query (the fused
+    projection sums in a different order), incl. the pipelined long-memory
+    variant and ragged key counts."""
+    O = ops()
+    bf = torch.bfloat16
+    H, D = dm // 64, 64
+    R, M = 5, 10
+    y = (torch.randn(M, dm, device=dev) * 2).to(bf)
+    g, be = torch.randn(dm, device=dev), torch.randn(dm, device=dev)
+    wq = (torch.randn(dm, dm, device=dev) / math.sqrt(dm)).to(bf)
+    bq = torch.randn(dm, device=dev) * 0.1
+    cache = torch.randn(R, 2, H, S, D, device=dev).to(bf)
+    req = (torch.arange(M, device=dev, dtype=torch.int32) // 2) % R
+    nk = torch.tensor([1, S, 17, S - 3, 1, 64, S // 2, 5, 1, S], device=dev, dtype=torch.int32)
+    kw = dict(H=H, D=D, row_stride=D, req_stride=2 * H * S * D, head_stride=S * D, scale=0.125)
+    xln = torch.empty_like(y)
+    O.layernorm(y, g, be, xln, torch.empty(M, device=dev), torch.empty(M, device=dev))
+    q = O.linear_decode(xln, wq, bq)
+    ref = torch.empty(M, dm, device=dev, dtype=bf)
+    O.attn_decode(q, cache, cache.view(-1)[H * S * D:], req, nk, ref, **kw)
+    got = torch.empty_like(ref)
+    x_out = torch.empty_like(y)
+    O.attn_decode_qln(y, g, be, wq, bq, cache, cache.view(-1)[H * S * D:], req, nk, got, x_out=x_out, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, xln)
+    assert rel_err(got, ref) < 2e-2, rel_err(got, ref)
+
+
 # ------------------------------------------------------------ fp8
 def _e4m3_ref(x, amax):
     """e4m3 bytes of x * (448 / amax): f32 scale by IEEE division, f32
