@@ -22,7 +22,7 @@ def main():
     m = bench.make_model(args, dev).eval()
     sess = {}
     with torch.no_grad():
-        for v in ("1", "0"):
+        for v in ("1", "0"):  # forced on / off (default "auto": on up to 64 rows)
             os.environ["SMER_DECODE_QLN"] = v
             s = DecodeSession(m, R, 1000, 600, use_graph=True)
             s.prefill(list(range(R)), [[4] * 1000 for _ in range(R)])
