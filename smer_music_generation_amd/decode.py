@@ -176,12 +176,13 @@ class DecodeSession:
         eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
         H, D, M = eng.H, eng.D, self.M
         pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
-        # the in-attention query projection re-reads the head's Wq slice per
-        # (row, head) block: a win up to 64 rows (R = 32: 329 vs 342 us per
-        # replayed step), a loss at 128 (R = 64: 484 vs 480;
-        # tools/decode_host_probe.py)
-        qln = os.environ.get("SMER_DECODE_QLN", "auto")
-        self._qln = D == 64 and d in (512, 768, 1024) and (qln == "1" or (qln == "auto" and M <= 64))
+        # The in-attention query projection re-reads the head's Wq slice per
+        # (row, head) block: 329 vs 342 us per replayed step at R = 32, 484
+        # vs 480 at R = 64 (tools/decode_host_probe.py).  It rounds q in a
+        # different order than the Linear, so the choice must not depend on
+        # the batch (a request's tokens may not depend on its batch-mates):
+        # on whenever the shape allows it.
+        self._qln = D == 64 and d in (512, 768, 1024) and os.environ.get("SMER_DECODE_QLN", "1") == "1"
         y_prev = n_prev = None
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
