@@ -227,6 +227,48 @@ __device__ __forceinline__ bf16x4 lds_read_tr16(const char* base, uint32_t byte_
   i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + byte_off));
   return __builtin_bit_cast(bf16x4, r);
 }
+// The same read as an asm statement, for k-loops whose next stage is in
+// flight by LDS-DMA (global_load_lds): hipcc cannot tell the intrinsic's LDS
+// read from the DMA's destination and waits vmcnt(0) before the first one of
+// every k-step (measured in the .s of every GEMM with a column-image
+// operand), so a stage's load never overlapped the MFMAs of the stage before.
+// The asm form is invisible to that bookkeeping AND to the lgkmcnt waits: the
+// caller retires the reads with lds_tr_retire() before using the registers.
+__device__ __forceinline__ bf16x4 lds_read_tr16_async(const char* base, uint32_t byte_off) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  const uint32_t a = (uint32_t)(uintptr_t)((lds_char*)(base + byte_off));
+  i16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return __builtin_bit_cast(bf16x4, r);
+}
+__device__ __forceinline__ uint4 lds_read_b128_async(const char* base, uint32_t byte_off) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  const uint32_t a = (uint32_t)(uintptr_t)((lds_char*)(base + byte_off));
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+// s_waitcnt lgkmcnt(n) for a compile-time n (asm immediates cannot come
+// from an unrolled loop variable)
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt is 4 bits");
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+  else static_assert(N == 0 || N == 2 || N == 4 || N == 6, "add the count");
+}
+// lgkmcnt(0), then every fragment register passes through an empty asm that
+// the MFMAs depend on, so none of them is scheduled above the wait.
+template <int NA, int NB>
+__device__ __forceinline__ void lds_tr_retire(bf16x8 (&a)[NA], bf16x8 (&b)[NB]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(b[i]));
+}
 __device__ __forceinline__ bf16x8 cat4(bf16x4 a, bf16x4 b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }

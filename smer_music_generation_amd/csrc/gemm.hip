@@ -222,8 +222,8 @@ __device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int la
     int u = (rbase >> 2) + p;
     int k0 = s * 32 + 8 * g + q;
     int k1 = k0 + 4;
-    bf16x4 lo = lds_read_tr16(buf, k0 * 256 + ((u ^ (4 * col_swz(k0))) << 3));
-    bf16x4 hi = lds_read_tr16(buf, k1 * 256 + ((u ^ (4 * col_swz(k1))) << 3));
+    bf16x4 lo = lds_read_tr16_async(buf, k0 * 256 + ((u ^ (4 * col_swz(k0))) << 3));
+    bf16x4 hi = lds_read_tr16_async(buf, k1 * 256 + ((u ^ (4 * col_swz(k1))) << 3));
     return cat4(lo, hi);
   }
 }
@@ -327,6 +327,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         for (int i = 0; i < 4; ++i) af[i] = frag<AK>(a_s, wm * 64 + i * 16, s, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+        if constexpr (!AK || !BKC) lds_tr_retire(af, bfr);  // asm transposing reads
         __builtin_amdgcn_sched_barrier(0);  // all 8 fragment reads, then the 16 MFMAs
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(256, 3) void gemm64_bf16_kernel(int M, int N, int K
         for (int i = 0; i < 2; ++i) af[i] = frag<true>(a_s, wm * 32 + i * 16, s, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
+        if constexpr (!BKC) lds_tr_retire(af, bfr);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -605,8 +607,8 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int
     const int u = (rbase >> 2) + p;
     const int k0 = s * 32 + 8 * g + q;
     const int k1 = k0 + 4;
-    bf16x4 lo = lds_read_tr16(buf, k0 * 512 + ((u ^ (4 * col_swz(k0))) << 3));
-    bf16x4 hi = lds_read_tr16(buf, k1 * 512 + ((u ^ (4 * col_swz(k1))) << 3));
+    bf16x4 lo = lds_read_tr16_async(buf, k0 * 512 + ((u ^ (4 * col_swz(k0))) << 3));
+    bf16x4 hi = lds_read_tr16_async(buf, k1 * 512 + ((u ^ (4 * col_swz(k1))) << 3));
     return cat4(lo, hi);
   }
 }
@@ -759,6 +761,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
         for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
 #pragma unroll
         for (int i = 0; i < 8; ++i) af[i] = g2_frag<AK>(a_s, wm * 128 + i * 16, s, lane);
+        if constexpr (!AK || !BKC) lds_tr_retire(af, bfr);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -808,6 +811,167 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
         }
       }
       smer_lds_barrier();  // LDS settled; stores left in flight
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradients on the 256x256 tile: dW (+)= dY^T X with K = tokens, both
+// operands M/N-contiguous (column images, transposing fragment reads).  Half
+// the L2->CU bytes per flop of the 128x128 kernel and twice the MFMA work per
+// stage to hide each stage's load behind (2 waves per SIMD x 2 k-steps x 32
+// MFMAs).  Deterministic split-K over K slices: work item = (slice, tile),
+// tiles of one slice adjacent so the blocks an XCD runs together read the
+// same dY / X rows through its L2; each slice writes an fp32 slab, reduced in
+// fixed order by splitk_reduce_kernel (or, unsplit, the epilogue adds into
+// dW).  Fused bias gradient on the first column tile: every wave sums two of
+// its eight A fragments per k-step with v_dot2c_f32_bf16 against ones (two
+// VGPRs; the row-sum MFMA variant spilled), lanes of a row reduced at the end.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rowsum_frag(bf16x8 v, float s) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(v, v, 0, 1), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(v, v, 2, 3), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(v, v, 4, 5), one, s, false);
+  s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(v, v, 6, 7), one, s, false);
+  return s;
+}
+
+__global__ __launch_bounds__(512, 1) void gemm256_wgrad_kernel(int M, int N, int K,
+                                                               const bf16* __restrict__ A, long lda,
+                                                               const bf16* __restrict__ B, long ldb,
+                                                               GemmEpi e, int ksplit, int kchunk,
+                                                               float* __restrict__ slabs,
+                                                               float* __restrict__ rowsum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wn_s = __builtin_amdgcn_readfirstlane(wn);  // wave-uniform branch below
+  const int nbm = (M + G2 - 1) / G2, nbn = (N + G2 - 1) / G2;
+  const int ntiles = nbm * nbn;
+  const int nwg = ntiles * ksplit;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int lin = xstart + jj;
+    const int split = lin / ntiles, wgid = lin % ntiles;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int tn = within / gsz;
+    const int m0 = (first_m + within % gsz) * G2, n0 = tn * G2;
+    const int k_begin = split * kchunk, k_end = min(K, k_begin + kchunk);
+    const int nk = (k_end - k_begin) / G2K;
+    const bool rsum = rowsum != nullptr && tn == 0;
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float rs0 = 0.f, rs1 = 0.f;
+
+    g2_glds<false>(smem, A, lda, M, m0, k_begin, tid);
+    g2_glds<false>(smem + G2_OP, B, ldb, N, n0, k_begin, tid);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // stage kt landed; stage kt-1 fully read
+      if (kt + 1 < nk) {
+        char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
+        g2_glds<false>(nb, A, lda, M, m0, k_begin + (kt + 1) * G2K, tid);
+        g2_glds<false>(nb + G2_OP, B, ldb, N, n0, k_begin + (kt + 1) * G2K, tid);
+      }
+      const char* a_s = smem + (kt & 1) * G2_STAGE;
+      const char* b_s = a_s + G2_OP;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 bfr[4], af[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<false>(b_s, wn * 64 + j * 16, s, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = g2_frag<false>(a_s, wm * 128 + i * 16, s, lane);
+        lds_tr_retire(af, bfr);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        if (rsum) {  // wave wn sums A fragments 2wn, 2wn+1 (rows of its 32)
+          if (wn_s == 0)      { rs0 = rowsum_frag(af[0], rs0); rs1 = rowsum_frag(af[1], rs1); }
+          else if (wn_s == 1) { rs0 = rowsum_frag(af[2], rs0); rs1 = rowsum_frag(af[3], rs1); }
+          else if (wn_s == 2) { rs0 = rowsum_frag(af[4], rs0); rs1 = rowsum_frag(af[5], rs1); }
+          else                { rs0 = rowsum_frag(af[6], rs0); rs1 = rowsum_frag(af[7], rs1); }
+        }
+      }
+    }
+    __syncthreads();  // all fragment reads done before the epilogue reuses LDS
+
+    if (rsum) {
+      // lane (g, c16) holds row c16's sum over its k subset: reduce over g
+      rs0 += __shfl_xor(rs0, 16); rs0 += __shfl_xor(rs0, 32);
+      rs1 += __shfl_xor(rs1, 16); rs1 += __shfl_xor(rs1, 32);
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = m0 + wm * 128 + (2 * wn + j) * 16 + lane;
+          const float v = j ? rs1 : rs0;
+          if (row < M) {
+            if (ksplit > 1) rowsum[(long)split * M + row] = v;
+            else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + v * e.alpha;
+          }
+        }
+      }
+    }
+
+    const int g = lane >> 4, c16 = lane & 15;
+    constexpr int EP_LD = G2 + 4;
+    float* ep = reinterpret_cast<float*>(smem);
+    float* slab = ksplit > 1 ? slabs + (long)split * M * N : nullptr;
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      if (wm == (pass >> 1)) {
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+          const int i = 4 * (pass & 1) + ii;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[(ii * 16 + 4 * g + r) * EP_LD + wn * 64 + j * 16 + c16] = acc[i][j][r];
+        }
+      }
+      smer_lds_barrier();
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int item = tid + 512 * c;  // 64 rows x 32 chunks of 8 columns
+        const int row = item >> 5, ch = item & 31;
+        const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
+        if (grow < M && gcol < N) {
+          float v[8];
+          const float4 a = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8);
+          const float4 b = *reinterpret_cast<const float4*>(ep + row * EP_LD + ch * 8 + 4);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          if (slab) {
+            const int valid = min(8, N - gcol);
+            float* dst = slab + (long)grow * N + gcol;
+            if (valid == 8 && (N & 3) == 0) {
+              *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+              *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+              for (int k = 0; k < valid; ++k) dst[k] = v[k];
+            }
+          } else {
+            epi_apply8(e, M, N, grow, gcol, v);
+          }
+        }
+      }
+      smer_lds_barrier();
     }
   }
 }
@@ -1096,6 +1260,25 @@ static int smer_splitk_depth() {
   return v;
 }
 
+// SMER_WGRAD256=1 moves the weight gradients to the 256x256 kernel (A/B);
+// SMER_WGRAD256_DEPTH: minimum K depth of its split-K slices
+static bool smer_wgrad256_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD256");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+static int smer_wgrad256_depth() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD256_DEPTH");
+    v = e ? std::max(64, atoi(e)) : 512;
+  }
+  return v;
+}
+
 // 16-row decode Linear workgroups (SMER_SKINNY16=0: 64-row strips; A/B runs)
 static bool smer_skinny16_enabled() {
   static int v = -1;
@@ -1180,6 +1363,40 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       auto kern = fast ? gemm256_bf16_kernel<AK, BKC, true> : gemm256_bf16_kernel<AK, BKC, false>;
       hipLaunchKernelGGL(kern, dim3(grid), dim3(512), G2_LDS, s,
                          M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+      return;
+    }
+  }
+  // weight gradients (both operands column images, pure fp32 output): the
+  // 256x256 tile when its split-K fills the chip with >= 512-deep slices
+  if (!AK && !BKC && K % G2K == 0 && ws && smer_wgrad256_enabled()) {
+    const bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr &&
+                         ((long)M * N) % 4 == 0;
+    const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
+    const long cus = smer_num_cus();
+    long ns = std::min<long>(cus / std::max<long>(1, t2), K / smer_wgrad256_depth());
+    ns = std::min<long>(ns, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
+    ns = std::max<long>(1, std::min<long>(ns, 64));
+    if (cf_only && t2 * ns * 4 >= 3 * cus) {
+      int kchunk = (int)(((K + ns - 1) / ns + G2K - 1) / G2K * G2K);
+      const int split = (K + kchunk - 1) / kchunk;
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipFuncSetAttribute((const void*)gemm256_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * G2_STAGE);
+        attr_set = true;
+      }
+      float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
+      const long nwg = t2 * split;
+      const int grid = nwg > cus ? (int)(cus & ~7L) : (int)nwg;
+      hipLaunchKernelGGL(gemm256_wgrad_kernel, dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
+                         (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
+                         split > 1 ? rs_part : rowsum);
+      if (split > 1) {
+        long n4 = ((long)M * N) / 4 + (rowsum ? M : 0);
+        hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,
+                           (const float*)ws, e.alpha, e.Cf, e.ldcf, e.accumulate,
+                           (const float*)rs_part, rowsum, e.rs_accumulate);
+      }
       return;
     }
   }
@@ -1502,16 +1719,36 @@ __device__ __forceinline__ void f8_glds(char* buf, const uint8_t* P, long ld, in
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(buf + chunk * 1024), 16, 0, 0);
   }
 }
-// lane (c16, g): row rbase + c16, k bytes [32g, 32g + 32) = chunks 2g, 2g + 1
-__device__ __forceinline__ i32x8 f8_frag(const char* buf, int rbase, int lane) {
-  const int g = lane >> 4, row = rbase + (lane & 15);
-  const int h = f8_swz(row);
-  const uint4 lo = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g) ^ h) << 4));
-  const uint4 hi = *reinterpret_cast<const uint4*>(buf + row * 128 + (((2 * g + 1) ^ h) << 4));
-  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-}
 __device__ __forceinline__ f32x4 mfma_f8(i32x8 a, i32x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+// lane (c16, g): row rbase + c16, k bytes [32g, 32g + 32) = chunks 2g, 2g + 1;
+// asm reads (lds_read_b128_async: hipcc otherwise waits vmcnt(0) for the next
+// stage's LDS-DMA before the first read of a k-step)
+__device__ __forceinline__ i32x8 f8_frag_async(const char* buf, int rbase, int lane) {
+  const int g = lane >> 4, row = rbase + (lane & 15);
+  const int h = f8_swz(row);
+  const uint4 lo = lds_read_b128_async(buf, row * 128 + (((2 * g) ^ h) << 4));
+  const uint4 hi = lds_read_b128_async(buf, row * 128 + (((2 * g + 1) ^ h) << 4));
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+// row fragment I of the k-step: read A fragment I + AHEAD, retire fragment I
+// (counted lgkmcnt: the 2 reads of each younger fragment stay in flight),
+// then its 4 MFMAs
+template <int I, int AHEAD>
+__device__ __forceinline__ void f8_kstep(f32x4 (&acc)[8][4], i32x8 (&af)[8], i32x8 (&bfr)[4],
+                                         const char* a_s, int wm, int lane) {
+  if constexpr (I + AHEAD < 8) af[I + AHEAD] = f8_frag_async(a_s, wm * 128 + (I + AHEAD) * 16, lane);
+  lds_wait<2 * ((7 - I) < AHEAD ? (7 - I) : AHEAD)>();
+  asm volatile("" : "+v"(af[I]));
+  if constexpr (I == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bfr[j]));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[I][j] = mfma_f8(af[I], bfr[j], acc[I][j]);
+  __builtin_amdgcn_sched_barrier(0);
 }
 }  // namespace
 
@@ -1583,17 +1820,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
       constexpr int AHEAD = FAST ? 1 : 3;  // FAST: bias registers leave no room for more
       i32x8 bfr[4], af[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(b_s, wn * 64 + j * 16, lane);
+      for (int j = 0; j < 4; ++j) bfr[j] = f8_frag_async(b_s, wn * 64 + j * 16, lane);
 #pragma unroll
-      for (int i = 0; i < AHEAD; ++i) af[i] = f8_frag(a_s, wm * 128 + i * 16, lane);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (i + AHEAD < 8) af[i + AHEAD] = f8_frag(a_s, wm * 128 + (i + AHEAD) * 16, lane);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_f8(af[i], bfr[j], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int i = 0; i < AHEAD; ++i) af[i] = f8_frag_async(a_s, wm * 128 + i * 16, lane);
+      f8_kstep<0, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<1, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<2, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<3, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<4, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<5, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<6, AHEAD>(acc, af, bfr, a_s, wm, lane);
+      f8_kstep<7, AHEAD>(acc, af, bfr, a_s, wm, lane);
     }
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
 

@@ -82,10 +82,15 @@ def test_gemm_splitk_wgrad(M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K,acc", [(512, 512, 32768, True), (1536, 512, 8192, False),
-                                       (309, 512, 4096, True), (200, 136, 96, True)])
+                                       (309, 512, 4096, True), (200, 136, 96, True),
+                                       (1000, 776, 32768, True), (4096, 4096, 512, False),
+                                       (4096, 4096, 512, True)])
 def test_gemm_wgrad_bias(M, N, K, acc):
     """Fused weight + bias gradient (split-K and unsplit, ragged M via a
-    padded dy row stride) equals dy^T x and the column sums of dy."""
+    padded dy row stride) equals dy^T x and the column sums of dy.  The
+    first two and the last three shapes run the 256x256 weight-gradient
+    kernel (ragged 256-tiles; unsplit when the tiles alone fill the chip),
+    the others the 128x128 one."""
     O = ops()
     ldm = (M + 7) // 8 * 8
     dy = torch.randn(K, ldm, device=dev).to(torch.bfloat16)
