@@ -138,7 +138,25 @@ class DecodeSession:
         cstride = 2 * H * self.Smax * D
         fused = dt == torch.bfloat16
         if fused:
-            self._run_fused_layers(x, scale, sstride, cstride)
+            if self.logits_t is None:
+                self.logits_t = torch.empty(M, eng.V, device=dev)
+            chains = self._chains()
+            if chains == 1:
+                self._run_fused_layers(x, scale, sstride, cstride, 0, M)
+                return
+            # Two independent request halves on two streams (graph branches),
+            # meant to overlap one half's HBM-bound cross attention with the
+            # other half's latency-bound Linears.  Every kernel computes a row
+            # the same way whatever rows share its launch (logits bit-identical
+            # either way).
+            h = 2 * (self.R // 2)
+            main = torch.cuda.current_stream(dev)
+            side = self._side_stream()
+            side.wait_stream(main)
+            self._run_fused_layers(x, scale, sstride, cstride, 0, h)
+            with torch.cuda.stream(side):
+                self._run_fused_layers(x, scale, sstride, cstride, h, M)
+            main.wait_stream(side)
             return
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
@@ -165,7 +183,21 @@ class DecodeSession:
         ops.gemm(out, W.fc_w, M=M, N=eng.V, K=d, out_f32=logits, bias=W.fc_b, dtype=dt)
         self.logits_t = logits
 
-    def _run_fused_layers(self, x, scale, sstride, cstride):
+    def _chains(self):
+        """Request chains per decode step.  SMER_DECODE_CHAINS=2 splits the
+        requests into two halves on two graph branches; measured slower
+        (C2 364 vs 326 us per replay, C5 888 vs 871: tools/decode_chain_probe.py),
+        so one chain is the default."""
+        if self.R < 2:
+            return 1
+        return 2 if os.environ.get("SMER_DECODE_CHAINS", "1") == "2" else 1
+
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.dev)
+        return self._side
+
+    def _run_fused_layers(self, x, scale, sstride, cstride, r0, r1):
         """bf16 decoder step with every post-norm LayerNorm fused into the
         prologue of the Linear that consumes it (ops.linear_decode_ln: LN1 ->
         cross Q, LN2 -> FFN1, LN3 -> next layer's QKV, final norm -> vocab
@@ -174,8 +206,10 @@ class DecodeSession:
         new K/V appended by the QKV epilogue: 7 launches per layer (11 in
         round 1)."""
         eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
-        H, D, M = eng.H, eng.D, self.M
-        pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
+        H, D, M = eng.H, eng.D, r1 - r0
+        pos_t, req_t, nks_t, nkc_t = (self.meta_t[0, r0:r1], self.meta_t[1, r0:r1],
+                                      self.meta_t[2, r0:r1], self.meta_t[3, r0:r1])
+        x = x[r0:r1]
         # The in-attention query projection re-reads the head's Wq slice per
         # (row, head) block: 329 vs 342 us per replayed step at R = 32, 484
         # vs 480 at R = 64 (tools/decode_host_probe.py).  It rounds q in a
@@ -216,9 +250,8 @@ class DecodeSession:
             y_prev = ops.linear(h, L.l2_w, L.l2_b, residual=x2)
             n_prev = L.n3
         x, _, _ = eng._ln(y_prev, n_prev, dt)  # last LN3; the final norm feeds the head below
-        logits = torch.empty(M, eng.V, device=dev) if self.logits_t is None else self.logits_t
-        ops.linear_decode_ln(x, W.dec_norm[0], W.dec_norm[1], W.fc_w, W.fc_b, out_f32=logits)
-        self.logits_t = logits
+        ops.linear_decode_ln(x, W.dec_norm[0], W.dec_norm[1], W.fc_w, W.fc_b,
+                             out_f32=self.logits_t[r0:r1])
 
     def _ensure_graph(self):
         if self.graph is not None or not self.use_graph:
