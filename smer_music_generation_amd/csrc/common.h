@@ -257,13 +257,24 @@ __device__ __forceinline__ void lds_wait() {
   else if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-  else static_assert(N == 0 || N == 2 || N == 4 || N == 6, "add the count");
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  else if constexpr (N == 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+  else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8 || N == 15, "add the count");
+}
+// Retire only the asm reads of one fragment set, issued before CNT younger
+// (compiler-visible) LDS reads whose waits hipcc places itself.
+template <int CNT, int NB>
+__device__ __forceinline__ void lds_tr_retire_older(bf16x8 (&b)[NB]) {
+  lds_wait<CNT>();
+#pragma unroll
+  for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(b[i]));
 }
 // lgkmcnt(0), then every fragment register passes through an empty asm that
 // the MFMAs depend on, so none of them is scheduled above the wait.
-template <int NA, int NB>
+// CNT > 0: only the reads older than the CNT youngest (LDS returns in order).
+template <int CNT = 0, int NA, int NB>
 __device__ __forceinline__ void lds_tr_retire(bf16x8 (&a)[NA], bf16x8 (&b)[NB]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_wait<CNT>();
 #pragma unroll
   for (int i = 0; i < NA; ++i) asm volatile("" : "+v"(a[i]));
 #pragma unroll

@@ -320,6 +320,36 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
       }
       const char* a_s = smem + cur * 2 * TILE_BYTES;
       const char* b_s = a_s + TILE_BYTES;
+      if constexpr (GL && !AK && !BKC) {
+        // weight gradients: both k-steps' fragments requested up front (32
+        // transposing reads); the second step's land under the first step's
+        // MFMAs.  lgkmcnt(15) retires the first 16 (LDS returns in order).
+        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af0[i] = frag<false>(a_s, wm * 64 + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf0[j] = frag<false>(b_s, wn * 64 + j * 16, 0, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af1[i] = frag<false>(a_s, wm * 64 + i * 16, 1, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf1[j] = frag<false>(b_s, wn * 64 + j * 16, 1, lane);
+        auto kstep = [&](bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+          if (rsum) {
+            accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
+            accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        lds_tr_retire<15>(af0, bf0);
+        kstep(af0, bf0);
+        lds_tr_retire<0>(af1, bf1);
+        kstep(af1, bf1);
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 af[4], bfr[4];
@@ -337,6 +367,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
           accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
           accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
         }
+      }
       }
       if (!GL && more) {
         stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
@@ -761,7 +792,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
         for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BKC>(b_s, wn * 64 + j * 16, s, lane);
 #pragma unroll
         for (int i = 0; i < 8; ++i) af[i] = g2_frag<AK>(a_s, wm * 128 + i * 16, s, lane);
-        if constexpr (!AK || !BKC) lds_tr_retire(af, bfr);
+        // dgrad: the 8 asm B reads are older than the 8 A row reads, whose
+        // waits hipcc places before each MFMA group itself
+        if constexpr (AK && !BKC) lds_tr_retire_older<8>(bfr);
+        else if constexpr (!AK || !BKC) lds_tr_retire(af, bfr);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
