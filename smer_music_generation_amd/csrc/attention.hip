@@ -220,14 +220,18 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     if (tid < KVB) kbias[0][tid] = key_bias(tid);
   }
   __syncthreads();
+  smer_vm_drain();  // prologue loads retired before the loop (common.h)
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
-    float nbias = 0.f;
+    // the next tile's padding byte is only loaded here and compared when it
+    // is staged below: comparing it at once made hipcc wait vmcnt(0) right
+    // behind the K / V prefetch, every tile
+    int npad = 0;
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
-      if (tid < KVB) nbias = key_bias((t + 1) * KVB + tid);
+      if (kp) npad = kp[min((t + 1) * KVB + lane, Lk - 1)];  // every lane: no exec-masked join
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
@@ -342,7 +346,8 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
-      if (tid < KVB) kbias[cur ^ 1][tid] = nbias;
+      asm volatile("" : "+v"(npad));  // keeps the compare (and its wait) here
+      if (tid < KVB) kbias[cur ^ 1][tid] = ((t + 1) * KVB + tid >= Lk || npad) ? -INFINITY : 0.f;
     }
     __syncthreads();
   }
@@ -445,9 +450,11 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
     tile_load<D>(ro, ob, lddo, t * KVB, Lq, tid);
     if (tid < KVB) {
-      int qq = t * KVB + tid;
-      rl = qq < Lq ? lb[qq] * LOG2E_F : INFINITY;
-      rd = qq < Lq ? db[qq] : 0.f;
+      // raw values, scaled / masked when staged: arithmetic on them here made
+      // hipcc wait for this tile's Q / dO prefetch right away
+      const int qq = t * KVB + tid;
+      rl = lb[min(qq, Lq - 1)];
+      rd = db[min(qq, Lq - 1)];
       if (DROP && !MSK) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
     }
     if (use_mask && tid < 4 * MCH) {
@@ -455,19 +462,22 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       rm = (q16 < nq16 && m_kt < nkt) ? m_base[q16 * nkt * 8] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int t) {
     tile_store<D>(rq, sm[buf][0], tid);
     tile_store<D>(ro, sm[buf][1], tid);
+    asm volatile("" : "+v"(rl), "+v"(rd));  // keeps the arithmetic below here
     if (tid < KVB) {
-      s_lse[buf][tid] = rl;
-      s_del[buf][tid] = rd;
+      const bool qv = t * KVB + tid < Lq;
+      s_lse[buf][tid] = qv ? rl * LOG2E_F : INFINITY;
+      s_del[buf][tid] = qv ? rd : 0.f;
       if (DROP && !MSK) s_rk[buf][tid] = rr;
     }
     if (use_mask && tid < 4 * MCH)
       reinterpret_cast<uint4*>(&s_msk[buf][0][0][0])[tid] = rm;
   };
-  if (t0 < n_qt) { load(t0); store(0); }
+  if (t0 < n_qt) { load(t0); store(0, t0); }
   __syncthreads();
+  smer_vm_drain();  // prologue loads retired before the loop (common.h)
   for (int t = t0; t < n_qt; ++t) {
     const int cur = (t - t0) & 1;
     const bool more = t + 1 < n_qt;
@@ -543,7 +553,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
         }
       }
     }
-    if (more) store(cur ^ 1);
+    if (more) store(cur ^ 1, t + 1);
     __syncthreads();
   }
 #pragma unroll
@@ -646,15 +656,16 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[0][0][0])[tid] = mask_load(0, tid);
   }
   __syncthreads();
+  smer_vm_drain();  // prologue loads retired before the loop (common.h)
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
-    float nbias = 0.f;
+    int npad = 0;  // compared when staged (see attn_fwd_bf16)
     uint4 nmask = make_uint4(0, 0, 0, 0);
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
-      if (tid < KVB) nbias = key_bias((t + 1) * KVB + tid);
+      if (kp) npad = kp[min((t + 1) * KVB + lane, Lk - 1)];  // every lane: no exec-masked join
       if (use_mask && tid < 32 * QG) nmask = mask_load(t + 1, tid);
     }
     const char* Ks = sm[cur][0];
@@ -723,7 +734,8 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
-      if (tid < KVB) kbias[cur ^ 1][tid] = nbias;
+      asm volatile("" : "+v"(npad));  // keeps the compare (and its wait) here
+      if (tid < KVB) kbias[cur ^ 1][tid] = ((t + 1) * KVB + tid >= Lk || npad) ? -INFINITY : 0.f;
       if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[cur ^ 1][0][0])[tid] = nmask;
     }
     __syncthreads();

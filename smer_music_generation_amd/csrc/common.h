@@ -303,6 +303,13 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // not its global stores (__syncthreads waits vmcnt(0): every pass would pay
 // the store round trip).  The asm memory clobbers keep the compiler from
 // moving memory operations across it.
+// s_waitcnt vmcnt(0) as a real instruction (hipcc's wait insertion counts
+// it, unlike an asm one).  Before a k-loop whose prologue loads were issued on
+// a path the compiler cannot prove the loop is entered from, its static merge
+// otherwise leaves those registers "pending" at the loop head and re-waits
+// them inside EVERY iteration -- where the wait also drains the prefetch of
+// the next tile.
+__device__ __forceinline__ void smer_vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 __device__ __forceinline__ void smer_lds_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xc07f);

@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         for (int j = 0; j < 4; ++j) bf1[j] = frag<false>(b_s, wn * 64 + j * 16, 1, lane);
         auto kstep = [&](bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
           __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
+  #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
             accr[0] = mfma16(wn ? af[2] : af[0], ones, accr[0]);
             accr[1] = mfma16(wn ? af[3] : af[1], ones, accr[1]);
           }
-          __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_sched_barrier(0);
         };
         lds_tr_retire<15>(af0, bf0);
         kstep(af0, bf0);
