@@ -108,7 +108,7 @@ static inline int ln_bwd_rows(int M) { return M <= 16384 ? LN_BWD_ROWS_SMALL : L
 // together (the rows are otherwise a chain of dependent HBM round trips at
 // 2 waves per SIMD).  Column partials for dgamma / dbeta accumulate in a
 // fixed row order (deterministic).
-template <typename T, bool DYF, int NC, int RB>
+template <typename T, bool DYF, int NC, int RB, bool PFB>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* __restrict__ dyv,
                                                      long lddy, const T* __restrict__ x, long ldx,
                                                      const float* __restrict__ mean,
@@ -131,22 +131,82 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
     for (int i = 0; i < 8; ++i) { pg[c][i] = 0.f; pb[c][i] = 0.f; }
   }
   const int r0 = blockIdx.x * rows_per_blk;
+  // bf16: the next batch's rows are fetched raw (16-B words, unclamped
+  // statistics) before this batch's math, so a wave keeps two batches in
+  // flight; every conversion / validity select happens at unpack time (a
+  // select right behind a load makes hipcc wait for it there)
+  constexpr bool PF = PFB && sizeof(T) == 2;  // PFB: several batches per wave (64-row blocks)
+  constexpr int DW = DYF ? 2 : 1;  // 16-B words of dy per 8 columns
+  uint4 px[PF ? RB : 1][NC], pd[PF ? RB : 1][NC][DW];
+  float pmu[PF ? RB : 1], prs[PF ? RB : 1];
+  auto fetch = [&](int rb) {
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int row = min(r0 + wave + 4 * (rb + u), M - 1);
+        pmu[u] = mean[row];
+        prs[u] = rstd[row];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int ch = lane + 64 * c;
+          if (ch < nch) {
+            px[u][c] = *reinterpret_cast<const uint4*>(x + (long)row * ldx + ch * 8);
+            if constexpr (DYF) {
+              const uint4* d = reinterpret_cast<const uint4*>((const float*)dyv + (long)row * lddy + ch * 8);
+              pd[u][c][0] = d[0];
+              pd[u][c][DW - 1] = d[1];
+            } else {
+              pd[u][c][0] = *reinterpret_cast<const uint4*>((const T*)dyv + (long)row * lddy + ch * 8);
+            }
+          }
+        }
+      }
+    }
+  };
+  if constexpr (PF) fetch(0);
   for (int rb = 0; rb < rows_per_blk / 4; rb += RB) {
     float xh[RB][NC][8], gd[RB][NC][8], mu[RB], rs[RB];
     bool ok[RB];
+    if constexpr (PF) {
 #pragma unroll
-    for (int u = 0; u < RB; ++u) {
-      const int row = r0 + wave + 4 * (rb + u);
-      ok[u] = row < M;
-      mu[u] = ok[u] ? mean[row] : 0.f;
-      rs[u] = ok[u] ? rstd[row] : 0.f;
+      for (int u = 0; u < RB; ++u) {
+        const int row = r0 + wave + 4 * (rb + u);
+        ok[u] = row < M;
+        mu[u] = ok[u] ? pmu[u] : 0.f;
+        rs[u] = ok[u] ? prs[u] : 0.f;
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int ch = lane + 64 * c;
-        if (ok[u] && ch < nch) {
-          Vec8<T>::load(x + (long)row * ldx + ch * 8, xh[u][c]);
-          if (DYF) Vec8<float>::load((const float*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
-          else Vec8<T>::load((const T*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
+        for (int c = 0; c < NC; ++c) {
+          const bf16x8 xv = __builtin_bit_cast(bf16x8, px[u][c]);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) xh[u][c][i] = (float)xv[i];
+          if constexpr (DYF) {
+            const float* f0 = reinterpret_cast<const float*>(&pd[u][c][0]);
+            const float* f1 = reinterpret_cast<const float*>(&pd[u][c][DW - 1]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { gd[u][c][i] = f0[i]; gd[u][c][4 + i] = f1[i]; }
+          } else {
+            const bf16x8 dv = __builtin_bit_cast(bf16x8, pd[u][c][0]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) gd[u][c][i] = (float)dv[i];
+          }
+        }
+      }
+      if (rb + RB < rows_per_blk / 4) fetch(rb + RB);
+    } else {
+#pragma unroll
+      for (int u = 0; u < RB; ++u) {
+        const int row = r0 + wave + 4 * (rb + u);
+        ok[u] = row < M;
+        mu[u] = ok[u] ? mean[row] : 0.f;
+        rs[u] = ok[u] ? rstd[row] : 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int ch = lane + 64 * c;
+          if (ok[u] && ch < nch) {
+            Vec8<T>::load(x + (long)row * ldx + ch * 8, xh[u][c]);
+            if (DYF) Vec8<float>::load((const float*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
+            else Vec8<T>::load((const T*)dyv + (long)row * lddy + ch * 8, gd[u][c]);
+          }
         }
       }
     }
@@ -403,10 +463,17 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   float ds = smer_drop_scale16(thr);
   float* part = params ? (float*)workspace : nullptr;
   SMER_REQUIRE(((uintptr_t)gamma & 15) == 0, "smer_layernorm_bwd: gamma must be 16-B aligned");
-#define LNB1(T, F, NC, RB)                                                                     \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, F, NC, RB>), dim3(nblk), dim3(256), 0, s, M, N, dy,     \
+#define LNB2(T, F, NC, RB, PF)                                                                 \
+  hipLaunchKernelGGL((ln_bwd_kernel<T, F, NC, RB, PF>), dim3(nblk), dim3(256), 0, s, M, N, dy, \
                      lddy, (const T*)x, ldx, mean, rstd, gamma, (T*)dx, lddx, (T*)dx_drop, ldxd, \
                      thr, seed, ds, part, rpb)
+  // next-batch prefetch only where a wave has more than one batch (32768
+  // rows: 32.6 -> 31.2 us; single-batch 16-row blocks measured slower with it)
+#define LNB1(T, F, NC, RB)                                          \
+  do {                                                              \
+    if (rpb / 4 > (RB)) LNB2(T, F, NC, RB, true);                   \
+    else LNB2(T, F, NC, RB, false);                                 \
+  } while (0)
 #define LNB(T, F)                                  \
   do {                                             \
     if (N <= 512) LNB1(T, F, 1, 4);                \
@@ -418,6 +485,7 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
 #undef LNB1
+#undef LNB2
   if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
     smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s, dbeta, N);
