@@ -196,8 +196,9 @@ def bench_infill(args, dev, rank):
     dt = time.perf_counter() - t0
     src_len = float(np.mean([len(r[0]) for r in reqs]))
     return {"tokens": st["tokens"], "steps": st["steps"], "seconds": dt,
-            "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s",
-                                                      "step_call_s")},
+            "phases_s": dict({k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s",
+                                                           "step_call_s")},
+                             **{k: round(v, 4) for k, v in st.get("decode_phases_s", {}).items()}),
             "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len,
             "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
             "roofline": infill_roofline(args, st)}
@@ -259,7 +260,8 @@ def bench_infill_c5(args, dev, rank):
             "p90_latency_s": float(np.percentile(lat, 90)),
             "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
             "roofline": infill_roofline(args, st),
-            "phases_s": {k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s")}}
+            "phases_s": dict({k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s")},
+                             **{k: round(v, 4) for k, v in st.get("decode_phases_s", {}).items()})}
 
 
 def _cpu_model():

@@ -204,6 +204,17 @@ int smer_grammar_greedy_step(int R, int V, const float* logits, long ldl, int32_
                              const uint8_t* cls, int eos, int m0, int trash_pos, int max_span,
                              const int32_t* src_len, int64_t* ids, int32_t* meta,
                              int32_t* out_tok, int cap, int32_t* alive, smer_stream_t stream);
+/* The same step with no per-step memset or host copy (the decode loop's
+ * replays then run back to back): ctl int32 [3] device words {live count,
+ * tickets, step} zeroed once by the caller; after the step its live count is
+ * written to ring[step % ring_n], pinned host memory the host reads once the
+ * step's event has completed.  Replaces the same generation.py:528-687 loop. */
+int smer_grammar_greedy_step_ring(int R, int V, const float* logits, long ldl, int32_t* state,
+                                  int nst, const int8_t* targets, int max_masks,
+                                  const uint8_t* keep, const uint8_t* cls, int eos, int m0,
+                                  int trash_pos, int max_span, const int32_t* src_len,
+                                  int64_t* ids, int32_t* meta, int32_t* out_tok, int cap,
+                                  int32_t* ctl, int32_t* ring, int ring_n, smer_stream_t stream);
 
 int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long ldx,
                        const float* gamma, const float* beta, float eps,

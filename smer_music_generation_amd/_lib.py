@@ -62,6 +62,9 @@ SIGNATURES = {
     "smer_fp8_scales": (c_int, [c_int, P, P, P, P, P]),
     "smer_grammar_greedy_step": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P, c_int,
                                          c_int, c_int, c_int, P, P, P, P, c_int, P, P]),
+    "smer_grammar_greedy_step_ring": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P,
+                                              c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P,
+                                              c_int, P]),
     "smer_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
                                    P, P]),
     "smer_layernorm_bwd_workspace": (c_size, [c_int, c_int]),

@@ -37,12 +37,31 @@ __device__ __forceinline__ int grammar_state(int flags, int len, int target, int
   return 11 + no_whole;
 }
 
+// RING: no memset / host copy per step.  ctl = {live count, tickets, step}
+// (device, zeroed once by the caller); every request's block takes a ticket
+// after adding itself to the live count, and the step's last block publishes
+// the count to ring[step % ring_n] (host-visible pinned memory) and resets
+// ctl for the next step.  The host reads the slot after the step's event.
+__device__ __forceinline__ void grammar_ring_ticket(int32_t* ctl, int32_t* ring, int ring_n, int R) {
+  const int t = __hip_atomic_fetch_add(&ctl[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == R - 1) {
+    const int a = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const int s = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ring[s % ring_n], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&ctl[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctl[2], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool RING>
 __global__ __launch_bounds__(64) void grammar_greedy_kernel(
     int R, int V, const float* __restrict__ logits, long ldl, int32_t* __restrict__ state,
     int nst, const int8_t* __restrict__ targets, int max_masks, const uint8_t* __restrict__ keep,
     const uint8_t* __restrict__ cls, int eos, int m0, int trash_pos, int max_span,
     const int32_t* __restrict__ src_len, int64_t* __restrict__ ids, int32_t* __restrict__ meta,
-    int M, int32_t* __restrict__ out_tok, int cap, int32_t* __restrict__ alive) {
+    int M, int32_t* __restrict__ out_tok, int cap, int32_t* __restrict__ alive,
+    int32_t* __restrict__ ring, int ring_n) {
   // one wave per request; the whole state vector is read in one load
   // (lane k <- st[k]) alongside the logits row, then broadcast
   const int r = blockIdx.x, lane = threadIdx.x;
@@ -56,7 +75,10 @@ __global__ __launch_bounds__(64) void grammar_greedy_kernel(
     lg[u] = i < V ? lr[i] : -INFINITY;
   }
   const int done0 = __shfl(sv, ST_DONE, 64);
-  if (done0) return;  // wave-uniform
+  if (done0) {  // wave-uniform
+    if (RING && lane == 0) grammar_ring_ticket(alive, ring, ring_n, R);
+    return;
+  }
   const int flags = __shfl(sv, ST_FLAGS, 64), len = __shfl(sv, ST_LEN, 64),
             midx = __shfl(sv, ST_MIDX, 64), nmask = __shfl(sv, ST_NMASK, 64),
             nowhole = __shfl(sv, ST_NOWHOLE, 64), cnt = __shfl(sv, ST_COUNT, 64),
@@ -138,8 +160,10 @@ __global__ __launch_bounds__(64) void grammar_greedy_kernel(
     st[ST_DONE] = 1;
   } else {
     st[ST_POS] = pos + nf;
-    atomicAdd(alive, 1);  // integer count: order-independent
+    if (RING) __hip_atomic_fetch_add(&alive[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else atomicAdd(alive, 1);  // integer count: order-independent
   }
+  if (RING) grammar_ring_ticket(alive, ring, ring_n, R);
 }
 
 extern "C" int smer_grammar_greedy_step(int R, int V, const float* logits, long ldl,
@@ -158,9 +182,36 @@ extern "C" int smer_grammar_greedy_step(int R, int V, const float* logits, long 
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(alive, 0, sizeof(int32_t), s) != hipSuccess)
     return smer_set_error(SMER_ERR_HIP, "smer_grammar_greedy_step: memset");
-  hipLaunchKernelGGL(grammar_greedy_kernel, dim3(R), dim3(64), 0, s, R, V,
+  hipLaunchKernelGGL(grammar_greedy_kernel<false>, dim3(R), dim3(64), 0, s, R, V,
                      logits, ldl, state, nst, targets, max_masks, keep, cls, eos, m0, trash_pos,
-                     max_span, src_len, ids, meta, 2 * R, out_tok, cap, alive);
+                     max_span, src_len, ids, meta, 2 * R, out_tok, cap, alive, nullptr, 0);
   SMER_CHECK_LAUNCH("smer_grammar_greedy_step");
+  return SMER_OK;
+}
+
+extern "C" int smer_grammar_greedy_step_ring(int R, int V, const float* logits, long ldl,
+                                             int32_t* state, int nst, const int8_t* targets,
+                                             int max_masks, const uint8_t* keep, const uint8_t* cls,
+                                             int eos, int m0, int trash_pos, int max_span,
+                                             const int32_t* src_len, int64_t* ids, int32_t* meta,
+                                             int32_t* out_tok, int cap, int32_t* ctl,
+                                             int32_t* ring, int ring_n, smer_stream_t stream) {
+  SMER_REQUIRE(R > 0 && V > 0 && nst >= 9 && max_masks > 0 && cap > 0 && ring_n > 0,
+               "smer_grammar_greedy_step_ring: sizes");
+  SMER_REQUIRE(ldl >= V, "smer_grammar_greedy_step_ring: logits row stride");
+  SMER_REQUIRE(logits && state && targets && keep && cls && src_len && ids && meta && out_tok && ctl && ring,
+               "smer_grammar_greedy_step_ring: null pointer");
+  SMER_REQUIRE(eos >= 0 && eos < V && m0 >= 0 && m0 < V && trash_pos > 0 && max_span > 1,
+               "smer_grammar_greedy_step_ring: token ids");
+  // the ring is pinned host memory: its device-side address
+  void* dring = nullptr;
+  if (hipHostGetDevicePointer(&dring, ring, 0) != hipSuccess || dring == nullptr) {
+    (void)hipGetLastError();
+    dring = ring;
+  }
+  hipLaunchKernelGGL(grammar_greedy_kernel<true>, dim3(R), dim3(64), 0, (hipStream_t)stream, R, V,
+                     logits, ldl, state, nst, targets, max_masks, keep, cls, eos, m0, trash_pos,
+                     max_span, src_len, ids, meta, 2 * R, out_tok, cap, ctl, (int32_t*)dring, ring_n);
+  SMER_CHECK_LAUNCH("smer_grammar_greedy_step_ring");
   return SMER_OK;
 }

@@ -354,8 +354,15 @@ class DecodeSession:
         self.g_cls = torch.from_numpy(np.ascontiguousarray(cls, dtype=np.uint8)).to(dev)
         self.g_srclen = torch.from_numpy(self.src_len.astype(np.int32)).to(dev)
         self.g_out = torch.zeros(self.R, cap, dtype=torch.int32, device=dev)
-        self.g_alive = torch.zeros(1, dtype=torch.int32, device=dev)
-        gargs = dict(eos=eos, m0=m0, trash_pos=self.Tmax - 1, max_span=max_span)
+        # live counts: the step's grammar kernel publishes its count into a
+        # pinned host ring itself (no per-step memset / D2H copy between the
+        # replays); SMER_GRAMMAR_RING=0: memset + copy per step (A/B)
+        use_ring = os.environ.get("SMER_GRAMMAR_RING", "1") != "0"
+        ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
+        rv = ring.numpy()
+        self.g_alive = torch.zeros(3 if use_ring else 1, dtype=torch.int32, device=dev)
+        gargs = dict(eos=eos, m0=m0, trash_pos=self.Tmax - 1, max_span=max_span,
+                     ring=ring if use_ring else None)
 
         def grammar():
             ops.grammar_greedy_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
@@ -364,9 +371,12 @@ class DecodeSession:
 
         # warm the decoder step eagerly (dummy rows only), then capture
         # step + grammar; the grammar kernel never runs outside the graph
+        import time
+        t_a = time.perf_counter()
         self._load_feeds([])
         self._run()
         torch.cuda.synchronize()
+        t_b = time.perf_counter()
         gs = torch.cuda.Stream()
         gs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(gs):
@@ -375,10 +385,10 @@ class DecodeSession:
                 self._run()
                 grammar()
         torch.cuda.current_stream().wait_stream(gs)
+        torch.cuda.synchronize()
+        t_c = time.perf_counter()
         self._load_feeds(feeds)
         max_steps = max([s.n_masks for s in spans] + [0]) * (max_span + 1) + 2
-        ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
-        rv = ring.numpy()
         inflight = []
         events = []
         steps = None
@@ -397,13 +407,17 @@ class DecodeSession:
                 raise RuntimeError("greedy_decode: no convergence within %d steps" % max_steps)
             g.replay()
             slot = issued % len(rv)
-            ring[slot:slot + 1].copy_(self.g_alive, non_blocking=True)
+            if not use_ring:
+                ring[slot:slot + 1].copy_(self.g_alive, non_blocking=True)
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             events.append(ev)
             inflight.append((issued, ev, slot))
             issued += 1
         torch.cuda.synchronize()
+        t_d = time.perf_counter()
+        # host seconds of this call's phases (bench / probes)
+        self.phase_s = {"warm_s": t_b - t_a, "capture_s": t_c - t_b, "loop_s": t_d - t_c}
         st = self.g_state.cpu().numpy()
         out = self.g_out.cpu().numpy()
         ids = [out[r, :min(int(st[r, 7]), cap)].tolist() for r in range(R)]

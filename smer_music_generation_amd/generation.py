@@ -476,5 +476,6 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,
                      "prefill_s": t2 - t1, "decode_s": t3 - t2, "step_call_s": t_dev,
                      "request_latency_s": latency, "kv_row_reads": kv_reads,
-                     "generated": [list(st.total) for st in spans]}
+                     "generated": [list(st.total) for st in spans],
+                     "decode_phases_s": dict(getattr(sess, "phase_s", {}))}
     return out

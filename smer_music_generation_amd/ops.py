@@ -390,7 +390,10 @@ def fp8_scales(amax_prev, qs, inv, amax_next):
 
 
 def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, out_tok, alive, *,
-                        eos, m0, trash_pos, max_span=100):
+                        eos, m0, trash_pos, max_span=100, ring=None):
+    """alive: int32 [1] live count (zeroed per step by a memset), or, with
+    `ring` (pinned host int32 [n]), int32 [3] control words zeroed once: the
+    step's live count lands in ring[step % n] with no per-step memset or copy."""
     R, nst = state.shape
     V = keep.shape[1]
     for t, dt in ((state, torch.int32), (targets, torch.int8), (keep, torch.uint8),
@@ -401,6 +404,14 @@ def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, o
     if logits.shape[0] < 2 * R or ids.shape[0] != 2 * R or meta.shape != (4, 2 * R) or \
             targets.shape[0] != R or keep.shape[0] != 13 or cls.shape[0] != V or src_len.shape[0] != R:
         raise RuntimeError("grammar_greedy_step: shape mismatch")
+    if ring is not None:
+        if ring.dtype != torch.int32 or not ring.is_pinned() or alive.numel() < 3:
+            raise RuntimeError("grammar_greedy_step: ring must be pinned int32, alive int32 [3]")
+        call("smer_grammar_greedy_step_ring", R, V, _p(logits), _ld(logits), _p(state), nst,
+             _p(targets), targets.shape[1], _p(keep), _p(cls), int(eos), int(m0), int(trash_pos),
+             int(max_span), _p(src_len), _p(ids), _p(meta), _p(out_tok), out_tok.shape[1],
+             _p(alive), ring.data_ptr(), ring.numel(), _stream())  # pinned host memory
+        return
     call("smer_grammar_greedy_step", R, V, _p(logits), _ld(logits), _p(state), nst, _p(targets),
          targets.shape[1], _p(keep), _p(cls), int(eos), int(m0), int(trash_pos), int(max_span),
          _p(src_len), _p(ids), _p(meta), _p(out_tok), out_tok.shape[1], _p(alive), _stream())
