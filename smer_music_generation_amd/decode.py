@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 
 import numpy as np
 import torch
@@ -318,6 +319,49 @@ class DecodeSession:
     # ------------------------------------------------------------------
     N_STATE = 12
 
+    def _capture_greedy(self, st, tg, keep, cls, cap, nm, eos, m0, lookahead, max_span, use_ring):
+        """Persistent grammar buffers + the captured (decoder step + grammar)
+        graph, reused by later greedy_decode calls of the same shapes."""
+        dev = self.dev
+        self.g_state = torch.from_numpy(st).to(dev)
+        self.g_targets = torch.from_numpy(tg).to(dev)
+        self.g_keep = torch.from_numpy(np.ascontiguousarray(keep, dtype=np.uint8)).to(dev)
+        self.g_cls = torch.from_numpy(np.ascontiguousarray(cls, dtype=np.uint8)).to(dev)
+        self.g_srclen = torch.from_numpy(self.src_len.astype(np.int32)).to(dev)
+        self.g_out = torch.zeros(self.R, cap, dtype=torch.int32, device=dev)
+        # live counts: the step's grammar kernel publishes its count into a
+        # pinned host ring itself (no per-step memset / D2H copy between the
+        # replays); SMER_GRAMMAR_RING=0: memset + copy per step (A/B)
+        ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
+        rv = ring.numpy()
+        self.g_alive = torch.zeros(3 if use_ring else 1, dtype=torch.int32, device=dev)
+        gargs = dict(eos=eos, m0=m0, trash_pos=self.Tmax - 1, max_span=max_span,
+                     ring=ring if use_ring else None)
+
+        def grammar():
+            ops.grammar_greedy_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
+                                    self.g_cls, self.g_srclen, self.ids_t, self.meta_t, self.g_out,
+                                    self.g_alive, **gargs)
+
+        # warm the decoder step eagerly (dummy rows only), then capture
+        # step + grammar; the grammar kernel never runs outside the graph
+        t_a = time.perf_counter()
+        self._load_feeds([])
+        self._run()
+        torch.cuda.synchronize()
+        t_b = time.perf_counter()
+        gs = torch.cuda.Stream()
+        gs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(gs):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs):
+                self._run()
+                grammar()
+        torch.cuda.current_stream().wait_stream(gs)
+        torch.cuda.synchronize()
+        t_c = time.perf_counter()
+        return g, ring, rv, t_a, t_b, t_c
+
     def greedy_decode(self, spans, keep, cls, *, eos, m0, lookahead=3, max_span=100):
         """Run the greedy infill loop of `spans` (generation._Span, one per
         request slot 0..len-1, freshly started, sources prefilled) entirely
@@ -348,45 +392,30 @@ class DecodeSession:
         st[R:, 5] = 1
         if not feeds:
             return [[] for _ in range(R)], 0, np.zeros(R, dtype=np.int32), []
-        self.g_state = torch.from_numpy(st).to(dev)
-        self.g_targets = torch.from_numpy(tg).to(dev)
-        self.g_keep = torch.from_numpy(np.ascontiguousarray(keep, dtype=np.uint8)).to(dev)
-        self.g_cls = torch.from_numpy(np.ascontiguousarray(cls, dtype=np.uint8)).to(dev)
-        self.g_srclen = torch.from_numpy(self.src_len.astype(np.int32)).to(dev)
-        self.g_out = torch.zeros(self.R, cap, dtype=torch.int32, device=dev)
-        # live counts: the step's grammar kernel publishes its count into a
-        # pinned host ring itself (no per-step memset / D2H copy between the
-        # replays); SMER_GRAMMAR_RING=0: memset + copy per step (A/B)
         use_ring = os.environ.get("SMER_GRAMMAR_RING", "1") != "0"
-        ring = torch.zeros(2 * lookahead + 2, dtype=torch.int32).pin_memory()
-        rv = ring.numpy()
-        self.g_alive = torch.zeros(3 if use_ring else 1, dtype=torch.int32, device=dev)
-        gargs = dict(eos=eos, m0=m0, trash_pos=self.Tmax - 1, max_span=max_span,
-                     ring=ring if use_ring else None)
-
-        def grammar():
-            ops.grammar_greedy_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
-                                    self.g_cls, self.g_srclen, self.ids_t, self.meta_t, self.g_out,
-                                    self.g_alive, **gargs)
-
-        # warm the decoder step eagerly (dummy rows only), then capture
-        # step + grammar; the grammar kernel never runs outside the graph
-        import time
-        t_a = time.perf_counter()
-        self._load_feeds([])
-        self._run()
-        torch.cuda.synchronize()
-        t_b = time.perf_counter()
-        gs = torch.cuda.Stream()
-        gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(gs):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=gs):
-                self._run()
-                grammar()
-        torch.cuda.current_stream().wait_stream(gs)
-        torch.cuda.synchronize()
-        t_c = time.perf_counter()
+        gkey = (nm, int(max_span), int(eos), int(m0), int(lookahead), use_ring, keep.shape, cls.shape)
+        gc = getattr(self, "_greedy", None)
+        if gc is not None and gc["key"] == gkey:
+            # the captured step + grammar graph of an earlier call with the
+            # same shapes: refresh its persistent inputs in place and replay
+            t_a = t_b = time.perf_counter()
+            self.eng.weights(self.dt)  # re-casts the bf16 weights in place if they moved
+            self.g_state.copy_(torch.from_numpy(st))
+            self.g_targets.copy_(torch.from_numpy(tg))
+            self.g_keep.copy_(torch.from_numpy(np.ascontiguousarray(keep, dtype=np.uint8)))
+            self.g_cls.copy_(torch.from_numpy(np.ascontiguousarray(cls, dtype=np.uint8)))
+            self.g_srclen.copy_(torch.from_numpy(self.src_len.astype(np.int32)))
+            self.g_out.zero_()
+            self.g_alive.zero_()
+            g, ring = gc["graph"], gc["ring"]
+            ring.zero_()
+            rv = ring.numpy()
+            torch.cuda.synchronize()
+            t_c = time.perf_counter()
+        else:
+            g, ring, rv, t_a, t_b, t_c = self._capture_greedy(st, tg, keep, cls, cap, nm, eos, m0,
+                                                             lookahead, max_span, use_ring)
+            self._greedy = {"key": gkey, "graph": g, "ring": ring}
         self._load_feeds(feeds)
         max_steps = max([s.n_masks for s in spans] + [0]) * (max_span + 1) + 2
         inflight = []

@@ -380,6 +380,35 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
 infill = generation_all
 
 
+# Warm decode sessions of generation_batch, one per (model, precision, R),
+# at most two kept: the KV caches, step buffers and the captured step +
+# grammar graph persist across calls (a serving process keeps them; capturing
+# costs ~10 ms at C2).  A cached session is reused when the call's sources and
+# prefix fit AND its cache capacities fall in the same decode-attention
+# variant class as a fresh session's would (>= 512 key rows: 8-wave blocks;
+# the kernels pick by capacity, and the variants sum in different orders), so
+# reuse never changes a token.
+_BATCH_SESSIONS = {}
+
+
+def _batch_session(model, R, Smax, Tmax, precision):
+    if precision is not None:
+        model.set_precision(precision)
+    key = (id(model), model.precision, R)
+    s = _BATCH_SESSIONS.get(key)
+    fits = (s is not None and s.model is model and s.Smax >= Smax and s.Tmax >= Tmax + 1
+            and (s.Smax >= 512) == (Smax >= 512) and (s.Tmax >= 512) == (Tmax + 1 >= 512))
+    if fits:
+        s.src_len[:] = 0
+        return s
+    s = DecodeSession(model, R, Smax, Tmax)
+    _BATCH_SESSIONS.pop(key, None)
+    while len(_BATCH_SESSIONS) >= 2:
+        _BATCH_SESSIONS.pop(next(iter(_BATCH_SESSIONS)))
+    _BATCH_SESSIONS[key] = s
+    return s
+
+
 def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logger=None,
                      max_tgt=None, precision=None, return_stats=False, device_grammar=True):
     """Decode many infill requests in lockstep on one KV-cached session.
@@ -403,7 +432,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     model.eval()
     tokens = steps = 0
     with torch.no_grad():
-        sess = DecodeSession(model, R, Smax, Tmax, precision=precision)
+        sess = _batch_session(model, R, Smax, Tmax, precision)
         t1 = time.perf_counter()
         sess.prefill(list(range(R)), [p[0] for p in preps])
         torch.cuda.synchronize()
