@@ -294,6 +294,32 @@ class _Span:
             self.logger.info(failmsg)
         return self.commit(idx)
 
+    def commit_all(self, seq):
+        """commit() over a whole emitted id sequence when nothing reads the
+        grammar flags between its ids (the device greedy grammar with no
+        redraw logger): the same tgt_inp / total / mask_idx / done, without
+        the per-token flag updates (only spec() reads them, and a finished
+        request never calls it again)."""
+        i2c = self.v.index2char
+        eos, ctrl = self.eos, self.all_controls
+        this_in, this_ev = self.this_in, self.this_ev
+        for idx in seq:
+            if idx in ctrl:
+                this_in += [idx, eos]
+                this_ev += [i2c(idx), '<eos>']
+            else:
+                this_in.append(idx)
+                this_ev.append(i2c(idx))
+            if this_in[-1] == eos or len(this_in) >= 100:
+                self.tgt_inp.extend(this_in[:-1])
+                self.total.extend(this_ev[:-1])
+                self.mask_idx += 1
+                if self.mask_idx >= self.n_masks:
+                    self.done = True
+                else:
+                    self._start_span()
+                    this_in, this_ev = self.this_in, self.this_ev
+
     def commit(self, idx):
         v = self.v
         idx = int(idx)
@@ -459,8 +485,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
                                for q, p in zip(seqs, preps)))
             for sp, seq in zip(spans, seqs):
                 if logger is None:  # no redraw report to log: commit only
-                    for idx in seq:
-                        sp.commit(idx)
+                    sp.commit_all(seq)
                 else:
                     for idx in seq:
                         _, chk, msg = sp.spec()

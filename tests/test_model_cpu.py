@@ -182,3 +182,28 @@ def test_device_grammar_mirror_matches_host_spans(seed):
 def allowed_ids_cached(v, flags):
     from smer_music_generation_amd.generation import allowed_ids
     return allowed_ids(v, **flags)
+
+
+def test_span_commit_all_equals_per_token_commit():
+    """The bulk replay of device-emitted ids (generation_batch, no logger)
+    ends in the same span state as committing them one at a time: ids drawn
+    at random from the whole vocabulary (controls, eos, 100-token spans)."""
+    from smer_music_generation_amd.generation import _Span
+    v = WordVocab(0, ['key', 'tensile', 'density', 'polyphony', 'occupation'])
+    ac = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
+    m0 = v.char2index('m_0')
+    rng = np.random.default_rng(3)
+    for trial in range(20):
+        n_masks = int(rng.integers(1, 5))
+        src = [4] * 10 + [m0] * n_masks
+        targets = ['r'] * n_masks
+        seq = []
+        a = _Span(v, src, targets, ac, False, True, None)
+        while not a.done and len(seq) < 2000:
+            r = rng.random()
+            idx = v.eos_index if r < 0.02 else (int(rng.choice(ac)) if r < 0.04 else int(rng.integers(0, 309)))
+            seq.append(idx)
+            a.commit(idx)
+        b = _Span(v, src, targets, ac, False, True, None)
+        b.commit_all(seq)
+        assert (a.tgt_inp, a.total, a.mask_idx, a.done) == (b.tgt_inp, b.total, b.mask_idx, b.done)
