@@ -229,6 +229,17 @@ int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int d
                        void* dx_drop, long ldxd, float drop_p, uint32_t seed,
                        float* dgamma, float* dbeta, int accumulate,
                        void* workspace, size_t ws_bytes, smer_stream_t stream);
+/* The same backward split in two, so the dgamma / dbeta column reduction
+ * (which only feeds the optimizer) can run on the weight-gradient stream:
+ * _partials writes dx (+ dx_drop) and the per-block column partials into
+ * `workspace`; _param_reduce sums them into dgamma / dbeta (nullable). */
+int smer_layernorm_bwd_partials(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
+                                const void* x, long ldx, const float* mean, const float* rstd,
+                                const float* gamma, void* dx, long lddx, void* dx_drop,
+                                long ldxd, float drop_p, uint32_t seed, void* workspace,
+                                size_t ws_bytes, smer_stream_t stream);
+int smer_layernorm_param_reduce(int M, int N, void* workspace, size_t ws_bytes, float* dgamma,
+                                float* dbeta, int accumulate, smer_stream_t stream);
 
 /* out[t] = dropout(table[ids[t]] * scale + pe[pos(t)]), pos(t) = positions
  * ? positions[t] : t % L.  table/pe fp32; out activation dtype. */

@@ -70,6 +70,9 @@ SIGNATURES = {
     "smer_layernorm_bwd_workspace": (c_size, [c_int, c_int]),
     "smer_layernorm_bwd": (c_int, [c_int, c_int, c_int, P, c_long, c_int, P, c_long, P, P, P, P,
                                    c_long, P, c_long, c_float, c_u32, P, P, c_int, P, c_size, P]),
+    "smer_layernorm_bwd_partials": (c_int, [c_int, c_int, c_int, P, c_long, c_int, P, c_long, P, P,
+                                            P, P, c_long, P, c_long, c_float, c_u32, P, c_size, P]),
+    "smer_layernorm_param_reduce": (c_int, [c_int, c_int, P, c_size, P, P, c_int, P]),
     "smer_embed_fwd": (c_int, [c_int, c_int, c_int, P, P, c_int, P, P, c_float, c_float, c_u32,
                                P, c_long, P]),
     "smer_embed_bwd_workspace": (c_size, [c_int, c_int, c_int]),

@@ -444,15 +444,16 @@ extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
   return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, 2 * N);
 }
 
-extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
-                                  const void* x, long ldx, const float* mean, const float* rstd,
-                                  const float* gamma, void* dx, long lddx, void* dx_drop,
-                                  long ldxd, float drop_p, uint32_t seed, float* dgamma,
-                                  float* dbeta, int accumulate, void* workspace, size_t ws_bytes,
-                                  smer_stream_t stream) {
+// reduce: 0 = write the per-block dgamma / dbeta partials only (reduced
+// later by smer_layernorm_param_reduce, e.g. on another stream)
+static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
+                       const void* x, long ldx, const float* mean, const float* rstd,
+                       const float* gamma, void* dx, long lddx, void* dx_drop, long ldxd,
+                       float drop_p, uint32_t seed, float* dgamma, float* dbeta, int accumulate,
+                       void* workspace, size_t ws_bytes, smer_stream_t stream, bool params,
+                       bool reduce) {
   SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_bwd: N % 8 == 0 and N <= 2048");
   SMER_REQUIRE(dx && dy && x && mean && rstd && gamma, "smer_layernorm_bwd: null pointer");
-  bool params = dgamma || dbeta;
   SMER_REQUIRE(!params || (workspace && ws_bytes >= smer_layernorm_bwd_workspace(M, N)),
                "smer_layernorm_bwd: workspace too small");
   if (M == 0) return SMER_OK;
@@ -486,16 +487,63 @@ extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long 
 #undef LNB
 #undef LNB1
 #undef LNB2
-  if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
+  if (reduce) {
+    if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
+      smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
+                             part + (size_t)nblk * 2 * N, s, dbeta, N);
+    else if (dgamma)
+      smer_col_reduce_launch(nblk, N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
+                             part + (size_t)nblk * 2 * N, s);
+    else if (dbeta)
+      smer_col_reduce_launch(nblk, N, part, (long)2 * N, (long)N, dbeta, accumulate, 1.f,
+                             part + (size_t)nblk * 2 * N, s);
+  }
+  SMER_CHECK_LAUNCH("smer_layernorm_bwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, int dy_f32,
+                                  const void* x, long ldx, const float* mean, const float* rstd,
+                                  const float* gamma, void* dx, long lddx, void* dx_drop,
+                                  long ldxd, float drop_p, uint32_t seed, float* dgamma,
+                                  float* dbeta, int accumulate, void* workspace, size_t ws_bytes,
+                                  smer_stream_t stream) {
+  return ln_bwd_impl(dtype, M, N, dy, lddy, dy_f32, x, ldx, mean, rstd, gamma, dx, lddx, dx_drop,
+                     ldxd, drop_p, seed, dgamma, dbeta, accumulate, workspace, ws_bytes, stream,
+                     dgamma || dbeta, true);
+}
+
+extern "C" int smer_layernorm_bwd_partials(int dtype, int M, int N, const void* dy, long lddy,
+                                           int dy_f32, const void* x, long ldx, const float* mean,
+                                           const float* rstd, const float* gamma, void* dx,
+                                           long lddx, void* dx_drop, long ldxd, float drop_p,
+                                           uint32_t seed, void* workspace, size_t ws_bytes,
+                                           smer_stream_t stream) {
+  SMER_REQUIRE(workspace, "smer_layernorm_bwd_partials: workspace required");
+  return ln_bwd_impl(dtype, M, N, dy, lddy, dy_f32, x, ldx, mean, rstd, gamma, dx, lddx, dx_drop,
+                     ldxd, drop_p, seed, nullptr, nullptr, 0, workspace, ws_bytes, stream, true,
+                     false);
+}
+
+extern "C" int smer_layernorm_param_reduce(int M, int N, void* workspace, size_t ws_bytes,
+                                           float* dgamma, float* dbeta, int accumulate,
+                                           smer_stream_t stream) {
+  SMER_REQUIRE(workspace && ws_bytes >= smer_layernorm_bwd_workspace(M, N),
+               "smer_layernorm_param_reduce: workspace too small");
+  if (M == 0 || (!dgamma && !dbeta)) return SMER_OK;
+  const int nblk = (M + ln_bwd_rows(M) - 1) / ln_bwd_rows(M);
+  float* part = (float*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  if (dgamma && dbeta)
     smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s, dbeta, N);
   else if (dgamma)
     smer_col_reduce_launch(nblk, N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s);
-  else if (dbeta)
+  else
     smer_col_reduce_launch(nblk, N, part, (long)2 * N, (long)N, dbeta, accumulate, 1.f,
                            part + (size_t)nblk * 2 * N, s);
-  SMER_CHECK_LAUNCH("smer_layernorm_bwd");
+  SMER_CHECK_LAUNCH("smer_layernorm_param_reduce");
   return SMER_OK;
 }
 

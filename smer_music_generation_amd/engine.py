@@ -436,6 +436,7 @@ class Engine:
 
         # vocab head
         side = self._wgrad_stream(dev, dt)
+        ps = side[0] if side is not None else None  # LayerNorm dgamma / dbeta reductions too
         wg = lambda *a, **kw: self._wgrad(side, *a, **kw)  # noqa: E731
         wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
@@ -443,7 +444,7 @@ class Engine:
         y_last, mo, ro = ctx.dec_last
         dy = torch.empty_like(y_last)
         ops.layernorm_bwd(g_out, y_last, mo, ro, W.dec_norm[0], dy, dgamma=G.dec_norm[0],
-                          dbeta=G.dec_norm[1])
+                          dbeta=G.dec_norm[1], param_stream=ps)
         if hook:
             self._join(side)
             hook("head")
@@ -458,7 +459,8 @@ class Engine:
             dy3 = torch.empty_like(y3)
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1])
+                              drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1],
+                              param_stream=ps)
             wg(dy3d, h, GL.l2_w, db=GL.l2_b)
             dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
             wg(dh, x2, GL.l1_w, db=GL.l1_b)
@@ -467,7 +469,8 @@ class Engine:
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx2, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+                              drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1],
+                              param_stream=ps)
             wg(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             doc = ops.linear_dgrad(dy2d, L.ca_ow)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
@@ -482,7 +485,8 @@ class Engine:
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+                              drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1],
+                              param_stream=ps)
             wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             do = ops.linear_dgrad(dy1d, L.sa_ow)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
@@ -504,14 +508,15 @@ class Engine:
         x_last, me, re = ctx.enc_last
         dx = torch.empty_like(x_last)
         ops.layernorm_bwd(dmem, x_last, me, re, W.enc_norm[0], dx, dgamma=G.enc_norm[0],
-                          dbeta=G.enc_norm[1])
+                          dbeta=G.enc_norm[1], param_stream=ps)
         for i in reversed(range(self.n_enc)):
             L, GL = W.enc[i], G.enc[i]
             (x_in, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2) = ctx.enc[i]
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1])
+                              drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1],
+                              param_stream=ps)
             wg(dy2d, h, GL.l2_w, db=GL.l2_b)
             dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
             wg(dh, x1, GL.l1_w, db=GL.l1_b)
@@ -519,7 +524,8 @@ class Engine:
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1])
+                              drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1],
+                              param_stream=ps)
             wg(dy1d, o, GL.out_w, db=GL.out_b)
             do = ops.linear_dgrad(dy1d, L.out_w)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)

@@ -425,11 +425,25 @@ def layernorm(x, gamma, beta, y, mean, rstd, eps=1e-5):
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, dx, *, dx_drop=None, drop_p=0.0, seed=0,
-                  dgamma=None, dbeta=None, accumulate=True):
+                  dgamma=None, dbeta=None, accumulate=True, param_stream=None):
+    """param_stream: run the dgamma / dbeta column reduction on that stream
+    (after this stream's LayerNorm kernel), off the dgrad chain."""
     lib = load()
     M, N = x.shape
     nbytes = lib.smer_layernorm_bwd_workspace(M, N) if (dgamma is not None or dbeta is not None) else 0
     ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=x.device)
+    if param_stream is not None and nbytes:
+        call("smer_layernorm_bwd_partials", dtype_code(x.dtype), M, N, _p(dy), _ld(dy),
+             int(dy.dtype == torch.float32 and x.dtype != torch.float32), _p(x), _ld(x), _p(mean),
+             _p(rstd), _p(gamma), _p(dx), _ld(dx), _p(dx_drop),
+             _ld(dx_drop) if dx_drop is not None else 0, float(drop_p), int(seed) & 0xFFFFFFFF,
+             _p(ws), nbytes, _stream())
+        param_stream.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(param_stream):
+            call("smer_layernorm_param_reduce", M, N, _p(ws), nbytes, _p(dgamma), _p(dbeta),
+                 int(accumulate), _stream())
+        ws.record_stream(param_stream)
+        return
     call("smer_layernorm_bwd", dtype_code(x.dtype), M, N, _p(dy), _ld(dy),
          int(dy.dtype == torch.float32 and x.dtype != torch.float32), _p(x), _ld(x), _p(mean),
          _p(rstd), _p(gamma), _p(dx), _ld(dx), _p(dx_drop),
