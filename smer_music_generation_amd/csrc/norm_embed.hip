@@ -313,6 +313,10 @@ __global__ void embed_fwd_kernel(int n_tok, int d, const int64_t* __restrict__ i
 constexpr int EMB_CHUNK = 512;  // tokens per workgroup in the per-vocab gather
 
 // part[chunk][v][:] = sum over tokens t of this chunk with id v of dx[t] * keep
+// A lane owns 8 consecutive columns (chunks lane, lane + 64: d <= 1024) and
+// reads them with one 16-B load per row; the matching rows of a 64-token
+// group are fetched up to 4 at a time (independent loads in flight) and
+// added in ascending token order, so the sums are those of a serial scan.
 template <typename T>
 __global__ __launch_bounds__(256) void embed_bwd_gather(
     int V, int d, const int64_t* __restrict__ ids0, const T* __restrict__ dx0, long ld0, int n0,
@@ -322,10 +326,12 @@ __global__ __launch_bounds__(256) void embed_bwd_gather(
   __shared__ float red[4][1024];
   const int v = blockIdx.x, chunk = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ncol = d / 64;  // columns per lane (d % 64 == 0, d <= 1024)
-  float acc[16];
+  const int nch = d >> 3;  // 8-column chunks (d % 8 == 0 for bf16 / fp32 vectors)
+  float acc[2][8];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[c][i] = 0.f;
   const int n = n0 + n1;
   const int t_begin = chunk * EMB_CHUNK + wave * (EMB_CHUNK / 4);
   for (int g0 = t_begin; g0 < t_begin + EMB_CHUNK / 4 && g0 < n; g0 += 64) {
@@ -334,28 +340,59 @@ __global__ __launch_bounds__(256) void embed_bwd_gather(
     if (t < n) hit = (t < n0 ? ids0[t] : ids1[t - n0]) == v;
     unsigned long long mask = __ballot(hit);
     while (mask) {
-      int b = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      int tt = g0 + b;
-      const bool s0 = tt < n0;
-      const int tl = s0 ? tt : tt - n0;
-      const uint32_t thr = s0 ? thr0 : thr1;
-      const uint32_t sd = s0 ? seed0 : seed1;
-      const float dsc = s0 ? ds0 : ds1;
+      int tt[4], cnt = 0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (i < ncol) {
-          int col = lane + 64 * i;
-          float g = s0 ? to_f32(dx0[(long)tl * ld0 + col]) : to_f32(dx1[(long)tl * ld1 + col]);
-          if (thr) g = smer_keep16(smer_rowkey(sd, (uint32_t)tl), thr, (uint32_t)col) ? g * dsc : 0.f;
-          acc[i] += g;
+      for (int k = 0; k < 4; ++k) {
+        tt[k] = -1;
+        if (mask) {
+          tt[k] = g0 + __ffsll((long long)mask) - 1;
+          mask &= mask - 1;
+          cnt = k + 1;
+        }
+      }
+      float g[4][2][8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < cnt) {
+          const bool s0 = tt[k] < n0;
+          const int tl = s0 ? tt[k] : tt[k] - n0;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int ch = lane + 64 * c;
+            if (ch < nch) {
+              if (s0) Vec8<T>::load(dx0 + (long)tl * ld0 + ch * 8, g[k][c]);
+              else Vec8<T>::load(dx1 + (long)tl * ld1 + ch * 8, g[k][c]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < cnt) {
+          const bool s0 = tt[k] < n0;
+          const int tl = s0 ? tt[k] : tt[k] - n0;
+          const uint32_t thr = s0 ? thr0 : thr1;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int ch = lane + 64 * c;
+            if (ch < nch) {
+              if (thr) smer_drop8(smer_rowkey(s0 ? seed0 : seed1, (uint32_t)tl), thr, s0 ? ds0 : ds1,
+                                  (uint32_t)(ch * 8), g[k][c]);
+#pragma unroll
+              for (int i = 0; i < 8; ++i) acc[c][i] += g[k][c][i];
+            }
+          }
         }
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i < ncol) red[wave][lane + 64 * i] = acc[i];
+  for (int c = 0; c < 2; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][ch * 8 + i] = acc[c][i];
+  }
   __syncthreads();
   float* dst = part + ((long)chunk * V + v) * d;
   for (int col = threadIdx.x; col < d; col += 256)
@@ -582,6 +619,9 @@ extern "C" int smer_embed_bwd(int dtype, int V, int d, float scale, const int64_
                               uint32_t seed1, float* dtable, void* workspace, size_t ws_bytes,
                               smer_stream_t stream) {
   SMER_REQUIRE(d % 64 == 0 && d <= 1024, "smer_embed_bwd: d % 64 == 0 and d <= 1024");
+  SMER_REQUIRE((!dx0 || (ld0 % 8 == 0 && ((uintptr_t)dx0 & 15) == 0)) &&
+                   (!dx1 || (ld1 % 8 == 0 && ((uintptr_t)dx1 & 15) == 0)),
+               "smer_embed_bwd: dx rows must be 16-B aligned (ld % 8 == 0)");
   SMER_REQUIRE(workspace && ws_bytes >= smer_embed_bwd_workspace(V, d, n0 + n1),
                "smer_embed_bwd: workspace too small");
   int n = n0 + n1;

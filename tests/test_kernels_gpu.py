@@ -455,10 +455,11 @@ def test_layernorm(dtype, M, N):
 
 
 # -------------------------------------------------------------- embedding
+@pytest.mark.parametrize("d", [128, 768])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_embedding(dtype):
+def test_embedding(dtype, d):
     O = ops()
-    V, d, B, L = 309, 128, 3, 50
+    V, B, L = 309, 3, 50
     table = torch.randn(V, d, device=dev)
     pe = torch.randn(2400, d, device=dev)
     ids = torch.randint(0, V, (B, L), device=dev)
