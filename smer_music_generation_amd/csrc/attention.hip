@@ -585,9 +585,9 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
     const bf16* __restrict__ k, long ldk, const bf16* __restrict__ v, long ldv,
     const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
-    const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
+    float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
     uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq,
-    const uint64_t* __restrict__ drop_mask) {
+    const uint64_t* __restrict__ drop_mask, const bf16* __restrict__ o, long ldo) {
   using C = AttnCfg<D>;
   constexpr int QB = 64 * QG;  // queries per block
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
@@ -620,14 +620,29 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     const int qi = q0w + gq * 16 + c16;
     const bool qvalid = qi < Lq;
     long row = (long)(b * Lq + min(qi, Lq - 1));
+    float dd = 0.f;
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
       qf[gq][s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
       of[gq][s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
+      if (o) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + row * ldo + h * D + s * 32 + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dd += (float)of[gq][s][e] * (float)ov[e];
+      }
     }
     // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
     lse2[gq] = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
-    dlt[gq] = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
+    if (o) {
+      // delta = rowsum(dO * O): the row's 4 lane groups hold D / 4 columns
+      // each; published for the dK / dV kernel, which runs after this one
+      dd += __shfl_xor(dd, 16);
+      dd += __shfl_xor(dd, 32);
+      dlt[gq] = qvalid ? dd : 0.f;
+      if (qvalid && g == 0) delta[(long)bh * Lq + qi] = dd;
+    } else {
+      dlt[gq] = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
+    }
     rowkey[gq] = (DROP && !MSK) ? smer_rowkey(seed, (uint32_t)(bh * Lq + qi)) : 0u;
   }
   const bf16* kb = k + (long)b * Lk * ldk + h * D;
@@ -1420,13 +1435,16 @@ extern "C" size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int L
   return delta;
 }
 
+#ifndef SMER_DQ_DELTA
+#define SMER_DQ_DELTA 1
+#endif
 template <int D>
 static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
                             long ldk, const void* v, long ldv, const void* dout, long lddo,
-                            const float* lse, const float* delta, const uint8_t* kpm, int causal,
+                            const float* lse, float* delta, const uint8_t* kpm, int causal,
                             float scale, uint32_t thr, uint32_t seed, float ds, void* dq,
                             long lddq, void* dk, long lddk, void* dv, long lddv,
-                            const uint64_t* mask, hipStream_t s) {
+                            const uint64_t* mask, const void* o, long ldo, hipStream_t s) {
   if (!thr) mask = nullptr;
   // two key groups per wave once there are enough blocks to fill the chip
   const bool kg2 = (long)((Lk + 127) / 128) * B * H >= 512 && D <= 64;
@@ -1441,14 +1459,20 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
   auto kdq = qg2 ? (cz ? SMER_BWD_PICK(attn_bwd_dq_bf16, 2, true) : SMER_BWD_PICK(attn_bwd_dq_bf16, 2, false))
                  : (cz ? SMER_BWD_PICK(attn_bwd_dq_bf16, 1, true) : SMER_BWD_PICK(attn_bwd_dq_bf16, 1, false));
 #undef SMER_BWD_PICK
+  // o != null: the dQ kernel forms delta = rowsum(dO * O) itself and runs
+  // first (no separate delta pass); else delta was written beforehand
+  auto launch_dq = [&] {
+    hipLaunchKernelGGL(kdq, dim3(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H), dim3(256), 0, s, B, H,
+                       Lq, Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
+                       (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
+                       (bf16*)dq, lddq, mask, (const bf16*)o, ldo);
+  };
+  if (o) launch_dq();
   hipLaunchKernelGGL(kdkdv, dim3(kg2 ? (Lk + 127) / 128 : (Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
                      (bf16*)dk, lddk, (bf16*)dv, lddv, mask);
-  hipLaunchKernelGGL(kdq, dim3(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
-                     Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
-                     (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
-                     (bf16*)dq, lddq, mask);
+  if (!o) launch_dq();
 }
 
 extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
@@ -1470,10 +1494,12 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   if (dtype == SMER_BF16) {
     SMER_REQUIRE(al16(q) && al16(k) && al16(v) && al16(dout), "smer_attn_bwd: 16-B alignment");
     SMER_REQUIRE(al16(o) && ldo % 8 == 0 && lddo % 8 == 0, "smer_attn_bwd: O/dO alignment");
-    launch_delta<bf16>(B, H, Lq, D, o, ldo, dout, lddo, delta, s);
-    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
-    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
-    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, s);
+    // SMER_DQ_DELTA=0 (A/B builds): separate delta pass, dK / dV kernel first
+    const void* of = SMER_DQ_DELTA ? o : nullptr;
+    if (!of) launch_delta<bf16>(B, H, Lq, D, o, ldo, dout, lddo, delta, s);
+    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
+    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
+    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     hipLaunchKernelGGL(attn_delta_scalar<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H,

@@ -301,6 +301,45 @@ def test_device_grammar_matches_host_loop(golden_dir, precision):
             assert [str(x) for x in got[0]] == rec["restored"]
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_warm_session_graph_reuse_and_ring_match_fresh(golden_dir, precision, monkeypatch):
+    """A warm call (session, KV caches and the captured step + grammar graph
+    left by an earlier call on other requests, inputs refreshed in place)
+    returns exactly what a fresh session returns, and so does the per-step
+    memset + copy live count (SMER_GRAMMAR_RING=0) instead of the ring the
+    grammar kernel writes."""
+    from smer_music_generation_amd import generation as G
+    from smer_music_generation_amd.synth import synth_events
+    from smer_music_generation_amd.vocab import WordVocab
+    z, meta = _golden(golden_dir)
+    m = _model(z, meta, precision)
+    v = WordVocab(0, CTRL)
+    ctl = _infill_cases(golden_dir)["all_controls"]
+    big = [(synth_events(70 + i, n_bars=7, n_tracks=3), [i % 3], [2, 3, 5]) for i in range(4)]
+    reqs = [(synth_events(80 + i, n_bars=4 + i, n_tracks=3), [(i + 1) % 3], [1, 2, 3] if i % 2 else [2])
+            for i in range(4)]
+
+    # same mask count as `big` (3 bars): the graph's key matches, so it is replayed
+    def run():
+        return G.generation_batch(m, [(list(e), t, b) for e, t, b in reqs], v, ctl, greedy=True)
+
+    G._BATCH_SESSIONS.clear()
+    fresh = run()
+    G._BATCH_SESSIONS.clear()
+    G.generation_batch(m, big, v, ctl, greedy=True)
+    sess = next(iter(G._BATCH_SESSIONS.values()))
+    graph = sess._greedy["graph"]
+    warm = run()
+    assert next(iter(G._BATCH_SESSIONS.values())) is sess and sess._greedy["graph"] is graph
+    monkeypatch.setenv("SMER_GRAMMAR_RING", "0")
+    noring = run()
+    for x, y, w in zip(fresh, warm, noring):
+        assert (x is None) == (y is None) == (w is None)
+        if x is not None:
+            assert [str(t) for t in x[0]] == [str(t) for t in y[0]] == [str(t) for t in w[0]]
+            assert x[1:] == y[1:] == w[1:]
+
+
 @pytest.mark.parametrize("precision,ltol,ptol", [("fp32", 1e-4, 1e-3), ("bf16", 3e-2, 0.35)])
 def test_three_fused_steps_track_oracle(precision, ltol, ptol):
     """Three Trainer steps (fused CE + backward + fused Adam) vs three oracle
