@@ -612,7 +612,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   auto mask_load = [&](int t, int ch) -> uint4 {
     return m_q16 < nq16 ? m_base[t * 8] : make_uint4(0, 0, 0, 0);
   };
-  bf16x8 qf[QG][C::NS], of[QG][C::NS];
+  bf16x8 qf[QG][C::NS], of[QG][C::NS], ovr[QG][C::NS];
   float lse2[QG], dlt[QG];
   uint32_t rowkey[QG];
 #pragma unroll
@@ -620,29 +620,16 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     const int qi = q0w + gq * 16 + c16;
     const bool qvalid = qi < Lq;
     long row = (long)(b * Lq + min(qi, Lq - 1));
-    float dd = 0.f;
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
       qf[gq][s] = *reinterpret_cast<const bf16x8*>(q + row * ldq + h * D + s * 32 + 8 * g);
       of[gq][s] = *reinterpret_cast<const bf16x8*>(dout + row * lddo + h * D + s * 32 + 8 * g);
-      if (o) {
-        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + row * ldo + h * D + s * 32 + 8 * g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dd += (float)of[gq][s][e] * (float)ov[e];
-      }
+      if (o) ovr[gq][s] = *reinterpret_cast<const bf16x8*>(o + row * ldo + h * D + s * 32 + 8 * g);
     }
-    // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
-    lse2[gq] = qvalid ? lse[(long)bh * Lq + qi] * LOG2E_F : INFINITY;
-    if (o) {
-      // delta = rowsum(dO * O): the row's 4 lane groups hold D / 4 columns
-      // each; published for the dK / dV kernel, which runs after this one
-      dd += __shfl_xor(dd, 16);
-      dd += __shfl_xor(dd, 32);
-      dlt[gq] = qvalid ? dd : 0.f;
-      if (qvalid && g == 0) delta[(long)bh * Lq + qi] = dd;
-    } else {
-      dlt[gq] = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
-    }
+    // raw lse, scaled once the first K / V tile's loads are in flight (a
+    // use right after the load would wait for it there)
+    lse2[gq] = lse[(long)bh * Lq + min(qi, Lq - 1)];
+    if (!o) dlt[gq] = qvalid ? delta[(long)bh * Lq + qi] : 0.f;
     rowkey[gq] = (DROP && !MSK) ? smer_rowkey(seed, (uint32_t)(bh * Lq + qi)) : 0u;
   }
   const bf16* kb = k + (long)b * Lk * ldk + h * D;
@@ -669,6 +656,30 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     tile_store<D>(rv, sm[0][1], tid);
     if (tid < KVB) kbias[0][tid] = key_bias(tid);
     if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[0][0][0])[tid] = mask_load(0, tid);
+  }
+#pragma unroll
+  for (int gq = 0; gq < QG; ++gq) {
+    // +inf lse past Lq: P = 0 there (that lane's dQ row is never written)
+    asm volatile("" : "+v"(lse2[gq]));
+    lse2[gq] = q0w + gq * 16 + c16 < Lq ? lse2[gq] * LOG2E_F : INFINITY;
+  }
+  if (o) {
+    // delta = rowsum(dO * O), formed once the first K / V tile's loads are
+    // in flight: the row's 4 lane groups hold D / 4 columns each; published
+    // for the dK / dV kernel, which runs after this one
+#pragma unroll
+    for (int gq = 0; gq < QG; ++gq) {
+      const int qi = q0w + gq * 16 + c16;
+      float dd = 0.f;
+#pragma unroll
+      for (int s = 0; s < C::NS; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dd += (float)of[gq][s][e] * (float)ovr[gq][s][e];
+      dd += __shfl_xor(dd, 16);
+      dd += __shfl_xor(dd, 32);
+      dlt[gq] = qi < Lq ? dd : 0.f;
+      if (qi < Lq && g == 0) delta[(long)bh * Lq + qi] = dd;
+    }
   }
   __syncthreads();
   smer_vm_drain();  // prologue loads retired before the loop (common.h)
