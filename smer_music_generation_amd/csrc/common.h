@@ -174,13 +174,13 @@ __device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
 // ln_fwd_kernel and the decode Linear's LayerNorm prologue so that both
 // produce the same bits.
 constexpr int LNR_MAXC = 4;
-template <typename T>
+template <typename T, int NC = LNR_MAXC>
 __device__ __forceinline__ void ln_row_stats(const T* __restrict__ xr, int N, float eps, int lane,
-                                             float (&v)[LNR_MAXC][8], float& mu, float& rs) {
+                                             float (&v)[NC][8], float& mu, float& rs) {
   const int nch = N >> 3;
   float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < LNR_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int ch = lane + 64 * c;
     if (ch < nch) {
       load8<T>(xr + ch * 8, 8, v[c]);
@@ -191,7 +191,7 @@ __device__ __forceinline__ void ln_row_stats(const T* __restrict__ xr, int N, fl
   mu = wave_sum(s) / N;
   float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < LNR_MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
     if (lane + 64 * c < nch)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {

@@ -34,8 +34,9 @@ template <> struct Vec8<float> {
 };
 }  // namespace
 
-// Q8: also the e4m3 copy of y (delayed scaling, common.h) for an fp8 GEMM
-template <typename T, bool Q8 = false>
+// Q8: also the e4m3 copy of y (delayed scaling, common.h) for an fp8 GEMM;
+// NC: 16-B chunks per lane the register arrays are sized for (N <= 512 * NC)
+template <typename T, bool Q8 = false, int NC = LN_MAXC>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __restrict__ x, long ldx,
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
@@ -47,9 +48,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
                                                      unsigned* __restrict__ amax = nullptr) {
   const int lane = threadIdx.x & 63;
   const int nch = N >> 3;
-  float gb[LN_MAXC][16];  // gamma | beta of the lane's chunks, issued before x
+  float gb[NC][16];  // gamma | beta of the lane's chunks, issued before x
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     const int ch = lane + 64 * c;
     if (ch < nch) {
       Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
@@ -61,10 +62,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
   // the Q8 form, whose capped grid loops so that the amax of the whole
   // tensor is committed by <= 2048 workgroups instead of one atomic per row)
   for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
-  float v[LNR_MAXC][8], mu, rs;
-  ln_row_stats<T>(x + (long)row * ldx, N, eps, lane, v, mu, rs);
+  float v[NC][8], mu, rs;
+  ln_row_stats<T, NC>(x + (long)row * ldx, N, eps, lane, v, mu, rs);
 #pragma unroll
-  for (int c = 0; c < LN_MAXC; ++c) {
+  for (int c = 0; c < NC; ++c) {
     int ch = lane + 64 * c;
     if (ch < nch) {
       float o[8];
@@ -93,6 +94,98 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
     __syncthreads();
     if (threadIdx.x < 64) smer_amax_commit(amax, lane < 4 ? wam[lane] : 0.f);
   }
+}
+
+// bf16 forward, RPW rows per wave: all RPW rows' loads are issued before
+// the first row's statistics (raw registers: a conversion right after a
+// load would make hipcc wait for it there), so a wave keeps RPW KiB of x in
+// flight instead of one row's; gamma / beta are read once per RPW rows.
+// NC = 16-B chunks per lane (N <= 512 * NC) sizes the register arrays, so a
+// d = 512 row costs a few dozen VGPRs.  Per-row arithmetic is ln_row_stats'
+// (bit-identical outputs).
+template <int RPW, int NC>
+__global__ __launch_bounds__(256) void ln_fwd_rows_kernel(int M, int N, const bf16* __restrict__ x,
+                                                          long ldx, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps,
+                                                          bf16* __restrict__ y, long ldy,
+                                                          float* __restrict__ mean,
+                                                          float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int nch = N >> 3;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= M) return;  // wave-uniform
+  bf16x8 raw[RPW][NC];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const long row = min(row0 + r, M - 1);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (lane + 64 * c < nch)
+        raw[r][c] = *reinterpret_cast<const bf16x8*>(x + row * ldx + (lane + 64 * c) * 8);
+  }
+  float gb[NC][16];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
+      Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    if (row >= M) break;  // wave-uniform
+    float v[NC][8], s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (lane + 64 * c < nch)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          v[c][i] = (float)raw[r][c][i];
+          s += v[c][i];
+        }
+    const float mu = wave_sum(s) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (lane + 64 * c < nch)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = v[c][i] - mu;
+          q += d * d;
+        }
+    const float rs = rsqrtf(wave_sum(q) / N + eps);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gb[c][i], gb[c][8 + i]);
+        Vec8<bf16>::store(y + (long)row * ldy + ch * 8, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+  }
+}
+
+// rows per wave of the bf16 forward: 1 from 16384 rows, else 4 (measured,
+// tools/ln_bench.py: 32768 x 512 13.3 us at 1, 14.0 at 2, 16.5 at 4, 18.8
+// for ln_fwd_kernel, whose arrays sized for N = 2048 cost 130 VGPRs; 8192
+// rows 9.2-9.8 us for all); SMER_LN_RPW = 1 / 2 / 4 forces it, 0 = the
+// one-row ln_fwd_kernel (A/B)
+static int ln_fwd_rpw(int M) {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("SMER_LN_RPW");
+    v = e ? atoi(e) : -1;
+    if (v != 0 && v != 1 && v != 2 && v != 4) v = -1;
+  }
+  return v >= 0 ? v : (M >= 16384 ? 1 : 4);
 }
 
 // rows per workgroup: 64 (16 per wave) for large M; 16 (one RB batch of 4
@@ -421,7 +514,15 @@ extern "C" int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long l
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((M + 3) / 4);
-  if (dtype == SMER_BF16)
+  const int rpw = dtype == SMER_BF16 ? ln_fwd_rpw(M) : 0;
+  if (rpw > 0) {
+    const int nc = N <= 512 ? 1 : N <= 1024 ? 2 : 4;
+#define LNF(R) (nc == 1 ? ln_fwd_rows_kernel<R, 1> : nc == 2 ? ln_fwd_rows_kernel<R, 2> : ln_fwd_rows_kernel<R, 4>)
+    auto kern = rpw == 1 ? LNF(1) : rpw == 2 ? LNF(2) : LNF(4);
+#undef LNF
+    hipLaunchKernelGGL(kern, dim3((M + 4 * rpw - 1) / (4 * rpw)), dim3(256), 0, s, M, N,
+                       (const bf16*)x, ldx, gamma, beta, eps, (bf16*)y, ldy, mean, rstd);
+  } else if (dtype == SMER_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16>, grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma,
                        beta, eps, (bf16*)y, ldy, mean, rstd);
   else if (dtype == SMER_F32)
@@ -445,8 +546,10 @@ extern "C" int smer_layernorm_fwd_fp8(int M, int N, const void* x, long ldx, con
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(std::min((M + 3) / 4, 2048));
-  hipLaunchKernelGGL((ln_fwd_kernel<bf16, true>), grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma,
-                     beta, eps, (bf16*)y, ldy, mean, rstd, (uint8_t*)q8, ldq, qs, amax);
+  auto kern = N <= 512 ? ln_fwd_kernel<bf16, true, 1> : N <= 1024 ? ln_fwd_kernel<bf16, true, 2>
+                                                                   : ln_fwd_kernel<bf16, true, 4>;
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, M, N, (const bf16*)x, ldx, gamma, beta, eps,
+                     (bf16*)y, ldy, mean, rstd, (uint8_t*)q8, ldq, qs, amax);
   SMER_CHECK_LAUNCH("smer_layernorm_fwd_fp8");
   return SMER_OK;
 }

@@ -421,7 +421,9 @@ def test_decode_attention(dtype, D, cap):
 
 # ------------------------------------------------------------ layernorm
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N", [(300, 512), (64, 768), (37, 64)])
+# bf16 forward: 4 rows per wave below 16384 rows (partial last workgroups), 1 above
+@pytest.mark.parametrize("M,N", [(300, 512), (64, 768), (37, 64), (16387, 512), (16400, 768),
+                                 (16390, 1536)])
 def test_layernorm(dtype, M, N):
     O = ops()
     x = (torch.randn(M, N, device=dev) * 3 + 1).to(dtype)
