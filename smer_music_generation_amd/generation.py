@@ -351,6 +351,14 @@ class _Span:
         return idx
 
 
+def _src_tokens(vocab, src):
+    """[vocab.index2char(int(t)) for t in src] (generation.py:685) through
+    one dict lookup per id instead of a method call and an int() each."""
+    table = getattr(vocab, "_idx2char", None)
+    get = table.get if isinstance(table, dict) else vocab.index2char
+    return [get(t) for t in (src.tolist() if hasattr(src, "tolist") else list(src))]
+
+
 def _prepare(events, vocab, tracks_to_generate, bars_to_generate):
     """generation.py:470-516: duration tables, mask targets, masked src."""
     name_to_time, time_to_name, times, bar_duration = durations_for_events(events)
@@ -397,8 +405,7 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
                     steps += 1
             if stats is not None:
                 stats["steps"] = steps
-        src_token = [vocab.index2char(int(t)) for t in src]
-        return restore_marked_input(src_token, st.total), mtn, mbn
+        return restore_marked_input(_src_tokens(vocab, src), st.total), mtn, mbn
     except Exception as e:  # reference behaviour (generation.py:695-696)
         print(e)
 
@@ -523,8 +530,7 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
         if st.n_masks == 0:
             out.append(None)
             continue
-        src_token = [vocab.index2char(int(t)) for t in p[0]]
-        out.append((restore_marked_input(src_token, st.total), p[1], p[2]))
+        out.append((restore_marked_input(_src_tokens(vocab, p[0]), st.total), p[1], p[2]))
     if return_stats:
         t3 = time.perf_counter()
         return out, {"tokens": tokens, "steps": steps, "prepare_s": t1 - t0,

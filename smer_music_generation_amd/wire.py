@@ -110,24 +110,24 @@ def restore_marked_input(src_token, generated_output):
     '<U9' array like the reference (tokens longer than 9 chars truncate).
     Raises IndexError when the source runs out of 'm_0' (reference behaviour
     of `np.where(...)[0][0]`)."""
-    src = [str(t)[:9] for t in np.array(src_token, dtype='<U9')]
-    gen = [str(t) for t in generated_output]
+    # (the reference's np.array(src_token) as '<U9': str() and truncation)
+    src = [t[:9] if type(t) is str else str(t)[:9] for t in src_token]
+    gen = [t if type(t) is str else str(t) for t in generated_output]
     starts = [i for i, t in enumerate(gen) if t == 'm_0']
     segs = []
     for j, s in enumerate(starts):
         e = starts[j + 1] if j + 1 < len(starts) else len(gen)
         segs.append(gen[s + 1:e])
-    out = []
-    it = iter(segs)
-    pending = len(segs)
-    for t in src:
-        if t == 'm_0' and pending > 0:
-            out.extend(next(it))
-            pending -= 1
-        else:
-            out.append(t)
-    if pending > 0:
+    # the first len(segs) 'm_0' of the source take the spans, in order
+    holes = [i for i, t in enumerate(src) if t == 'm_0'][:len(segs)]
+    if len(holes) < len(segs):
         raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+    out, prev = [], 0
+    for i, seg in zip(holes, segs):
+        out += src[prev:i]
+        out += seg
+        prev = i + 1
+    out += src[prev:]
     return np.array(out, dtype='<U9')
 
 
