@@ -356,13 +356,13 @@ def _src_tokens(vocab, src):
     one dict lookup per id instead of a method call and an int() each."""
     table = getattr(vocab, "_idx2char", None)
     get = table.get if isinstance(table, dict) else vocab.index2char
-    return [get(t) for t in (src.tolist() if hasattr(src, "tolist") else list(src))]
+    return list(map(get, src.tolist() if hasattr(src, "tolist") else list(src)))
 
 
 def _prepare(events, vocab, tracks_to_generate, bars_to_generate):
     """generation.py:470-516: duration tables, mask targets, masked src."""
     name_to_time, time_to_name, times, bar_duration = durations_for_events(events)
-    n_bars = sum(1 for e in events if e == 'bar')
+    n_bars = events.count('bar') if isinstance(events, list) else sum(1 for e in events if e == 'bar')
     target, tracks = mask_targets(events, tracks_to_generate, bars_to_generate)
     if bars_to_generate[-1] >= n_bars:
         events = fill_empty_bars(events, bars_to_generate[-1] - n_bars + 1, bar_duration,

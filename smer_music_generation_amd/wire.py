@@ -13,6 +13,7 @@ tests/golden/mask_bar_and_track.json and infill_micro.json).
 """
 from __future__ import annotations
 
+import operator
 import re
 
 import numpy as np
@@ -34,7 +35,8 @@ def bar_track_spans(events):
     Same grouping as `generation.py:258-292`."""
     names = set(track_names_of(events))
     n_tracks = len(names)
-    marks = [i for i, t in enumerate(events) if t == 'bar' or t in names]
+    heads = names | {'bar'}
+    marks = [i for i, t in enumerate(events) if t in heads]
     marks.append(len(events))
     out = []
     cur = []
@@ -79,9 +81,10 @@ def _to_ids(vocab, toks):
     token (char2index's per-call overhead dominated the host preparation)
     unless some token is unknown (then char2index itself, for its report)."""
     table = vocab._char2idx
-    if set(toks) - table.keys():
+    try:
+        return np.array(list(map(table.__getitem__, toks)), dtype=np.int64)
+    except KeyError:
         return np.array([vocab.char2index(t) for t in toks])
-    return np.fromiter((table[t] for t in toks), dtype=np.int64, count=len(toks))
 
 
 def decoder_targets(event, vocab, mask_tracks, mask_bars):
@@ -104,6 +107,9 @@ def decoder_targets(event, vocab, mask_tracks, mask_bars):
     return out
 
 
+_FIRST9 = operator.itemgetter(slice(0, 9))
+
+
 def restore_marked_input(src_token, generated_output):
     """Splice each generated span (the text between successive 'm_0' in
     `generated_output`) into the successive 'm_0' of `src_token`.  Returns a
@@ -111,7 +117,10 @@ def restore_marked_input(src_token, generated_output):
     Raises IndexError when the source runs out of 'm_0' (reference behaviour
     of `np.where(...)[0][0]`)."""
     # (the reference's np.array(src_token) as '<U9': str() and truncation)
-    src = [t[:9] if type(t) is str else str(t)[:9] for t in src_token]
+    if set(map(type, src_token)) <= {str}:
+        src = list(map(_FIRST9, src_token))
+    else:
+        src = [str(t)[:9] for t in src_token]
     gen = [t if type(t) is str else str(t) for t in generated_output]
     starts = [i for i, t in enumerate(gen) if t == 'm_0']
     segs = []
@@ -119,9 +128,14 @@ def restore_marked_input(src_token, generated_output):
         e = starts[j + 1] if j + 1 < len(starts) else len(gen)
         segs.append(gen[s + 1:e])
     # the first len(segs) 'm_0' of the source take the spans, in order
-    holes = [i for i, t in enumerate(src) if t == 'm_0'][:len(segs)]
-    if len(holes) < len(segs):
-        raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+    holes, at = [], 0
+    for _ in segs:
+        try:
+            at = src.index('m_0', at)
+        except ValueError:
+            raise IndexError("index 0 is out of bounds for axis 0 with size 0") from None
+        holes.append(at)
+        at += 1
     out, prev = [], 0
     for i, seg in zip(holes, segs):
         out += src[prev:i]
