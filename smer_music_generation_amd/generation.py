@@ -54,10 +54,13 @@ def softmax_with_temperature(logits, temperature):
 
 
 def weighted_sampling(probs):
-    probs /= sum(probs)
-    sorted_probs = np.sort(probs)[::-1]
+    # the reference's builtin sum() adds left to right from 0: the last
+    # element of the (sequential) cumulative sum is that number exactly, in
+    # 1/12 of the time; probs[argsort] holds np.sort's values (ties are
+    # equal values), so one sort serves both
+    probs /= np.add.accumulate(probs)[-1]
     sorted_index = np.argsort(probs)[::-1]
-    return np.random.choice(sorted_index, size=1, p=sorted_probs)[0]
+    return np.random.choice(sorted_index, size=1, p=probs[sorted_index])[0]
 
 
 _FLAG_NAMES = ("no_pitch", "no_duration", "no_rest", "no_whole_duration", "no_eos",
@@ -70,7 +73,7 @@ def allowed_ids(vocab, **flags):
     """Boolean [V]: logits `sampling` keeps (others become -100).  The
     reference's `no_control` test (`i in dict.values()`) never matches
     (SURVEY Q1), so it is a no-op here too."""
-    key = (id(vocab),) + tuple(bool(flags.get(f, False)) for f in _FLAG_NAMES)
+    key = (id(vocab),) + tuple(map(bool, map(flags.get, _FLAG_NAMES)))
     hit = _MASK_CACHE.get(key)
     if hit is not None:
         return hit

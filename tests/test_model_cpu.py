@@ -207,3 +207,31 @@ def test_span_commit_all_equals_per_token_commit():
         b = _Span(v, src, targets, ac, False, True, None)
         b.commit_all(seq)
         assert (a.tgt_inp, a.total, a.mask_idx, a.done) == (b.tgt_inp, b.total, b.mask_idx, b.done)
+
+
+def test_weighted_sampling_draws_equal_reference_formulation():
+    """generation.weighted_sampling (cumulative-sum normaliser, one argsort)
+    draws exactly what the reference's builtin sum() + np.sort + np.argsort
+    formulation draws (generation.py:56-61) under the same numpy seed,
+    including masked logits (many tied probabilities)."""
+    import numpy as np
+    from smer_music_generation_amd.generation import weighted_sampling
+
+    def ref(probs):
+        probs /= sum(probs)
+        sorted_probs = np.sort(probs)[::-1]
+        sorted_index = np.argsort(probs)[::-1]
+        return np.random.choice(sorted_index, size=1, p=sorted_probs)[0]
+
+    rng = np.random.default_rng(1)
+    for i in range(500):
+        x = rng.standard_normal(309) * rng.uniform(0.1, 8)
+        if i % 3 == 0:
+            x[rng.integers(0, 309, 60)] = -100.0
+        p = np.exp(x)
+        p = p / np.sum(p)
+        np.random.seed(i)
+        a = ref(p.copy())
+        np.random.seed(i)
+        b = weighted_sampling(p.copy())
+        assert a == b, i
