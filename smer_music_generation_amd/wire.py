@@ -35,8 +35,19 @@ def bar_track_spans(events):
     Same grouping as `generation.py:258-292`."""
     names = set(track_names_of(events))
     n_tracks = len(names)
-    heads = names | {'bar'}
-    marks = [i for i, t in enumerate(events) if t in heads]
+    # positions of every 'bar' / track token: one C-level list.index scan
+    # per head kind (a few hundred hits) instead of a Python pass per token
+    seq = events if isinstance(events, list) else list(events)
+    marks = []
+    for head in names | {'bar'}:
+        i = -1
+        try:
+            while True:
+                i = seq.index(head, i + 1)
+                marks.append(i)
+        except ValueError:
+            pass
+    marks.sort()
     marks.append(len(events))
     out = []
     cur = []
