@@ -26,7 +26,7 @@ N_TRACK_CONTROLS = 3  # density, occupation, polyphony (generation.py:249)
 
 def track_names_of(events):
     # the regex runs over the distinct tokens (a few hundred), not the song
-    return sorted(t for t in set(events) if _TRACK_RE.match(t))
+    return sorted(t for t in set(events) if t.startswith('track_') and _TRACK_RE.match(t))
 
 
 def bar_track_spans(events):
