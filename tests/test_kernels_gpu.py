@@ -1,6 +1,7 @@
 """Kernel-level parity of the HIP C-ABI against fp32 torch math on the GPU
 (floating-point kernels: torch fp32 is the reference of the same op)."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -818,3 +819,24 @@ def test_gemm64_mid_size_epilogues(M, N, K, bk):
     ref = torch.where(R.float() > 0, base * 1.5, torch.zeros_like(base))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < 2e-2
+
+
+def test_layernorm_fwd_rows_kernel_bit_identical_to_one_row_kernel(tmp_path):
+    """The bf16 LayerNorm forward's rows-per-wave kernel (register arrays
+    sized for the row width) returns the one-row ln_fwd_kernel's bits, for
+    each rows-per-wave setting (the setting is read once per process:
+    tools/ln_fwd_bits.py runs once per SMER_LN_RPW value)."""
+    import subprocess
+    import sys
+    import numpy as np
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for rpw in ("0", "1", "2", "4"):
+        f = str(tmp_path / ("ln%s.npz" % rpw))
+        env = dict(os.environ, SMER_LN_RPW=rpw)
+        subprocess.run([sys.executable, os.path.join(root, "tools", "ln_fwd_bits.py"), f],
+                       env=env, check=True, timeout=180)
+        outs[rpw] = np.load(f)
+    for rpw in ("1", "2", "4"):
+        for k in outs["0"].files:
+            assert np.array_equal(outs["0"][k], outs[rpw][k]), (rpw, k)
