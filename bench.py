@@ -55,30 +55,65 @@ def make_model(args, dev, precision="bf16"):
     return m.to(dev)
 
 
-def bench_train(args, dev, rank, world, precision="bf16"):
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def timed_steps(step, steps, warmup, dev, world):
+    """The bench contract's timed region: W untimed warmup steps, then
+    exactly K steps bracketed by barrier + device synchronize on both sides;
+    returns (seconds of this rank, last step's result)."""
+    out = None
+    for _ in range(warmup):
+        out = step()
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    _sync(dev)
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0, out
+
+
+def max_over_ranks(x, dev, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.item()
+
+
+def params_in_sync(model, dev, world):
+    """True when every rank holds bit-identical parameters (after the
+    Trainer's rank-0 broadcast): each rank's flat buffer hashed to two
+    float64 sums, gathered and compared."""
+    if world == 1:
+        return True
+    flat = model.flat_parameters().detach()
+    idx = torch.arange(flat.numel(), device=flat.device, dtype=torch.float64) % 1021 + 1
+    h = torch.stack([flat.double().sum(), (flat.double() * idx).sum()]).to(dev)
+    allh = [torch.zeros_like(h) for _ in range(world)]
+    dist.all_gather(allh, h)
+    return all(torch.equal(allh[0], x) for x in allh[1:])
+
+
+def bench_train(args, dev, rank, world, precision="bf16", grad_wire=None):
     from smer_music_generation_amd import ops
     from smer_music_generation_amd.synth import synth_training_batch
     from smer_music_generation_amd.train import Trainer
     from smer_music_generation_amd.vocab import WordVocab
     v = WordVocab(0, CTRL)
     m = make_model(args, dev, precision)
-    tr = Trainer(m, v, lr=1e-4)
+    tr = Trainer(m, v, lr=1e-4, grad_wire_dtype=grad_wire)
+    in_sync = params_in_sync(m, dev, world)
     b = synth_training_batch(1000 + rank, v, args.batch, args.seq, args.tgt)
     bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
-    for _ in range(args.warmup):
-        tr.step(bt)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = tr.step(bt)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
+    dt, loss = timed_steps(lambda: tr.step(bt), args.steps, args.warmup, dev, world)
     # The per-launch GEMM timing (HIP events around every smer_gemm call)
     # runs over a second, separate set of K steps so that the event records
     # do not slow the timed steps above.  Those steps run the weight
@@ -102,16 +137,14 @@ def bench_train(args, dev, rank, world, precision="bf16"):
                 del os.environ["SMER_WGRAD_OVERLAP"]
             else:
                 os.environ["SMER_WGRAD_OVERLAP"] = prev
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+    dt = max_over_ranks(dt, dev, world)
     tokens = world * args.batch * (args.seq + args.tgt) * args.steps
     flops_sample = train_flops_per_sample(args.layers, args.d_model, args.ff, 309, args.seq, args.tgt)
     step_flops = 3.0 * flops_sample * args.batch  # per GPU: fwd + 2x bwd
     res = {"tokens_per_s": tokens / dt, "ms_per_step": 1000 * dt / args.steps,
            "tgt_tokens_per_s": world * args.batch * args.tgt * args.steps / dt,
-           "loss": float(loss.item()),
+           "loss": float(loss.item()), "params_in_sync_at_init": in_sync,
+           "grad_allreduce_dtype": "bf16" if grad_wire == torch.bfloat16 else "fp32",
            "step_tflops_per_gpu": step_flops / (dt / args.steps) / 1e12,
            "mfma_frac_whole_step": step_flops / (dt / args.steps) / 1e12 / BF16_PEAK_TFLOPS}
     if timer is not None:
@@ -404,7 +437,71 @@ def parse_args(argv=None):
     ap.add_argument("--c5-seq", dest="c5_seq", type=int, default=4096)
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--no-roofline", dest="roofline", action="store_false")
+    ap.add_argument("--grad-wire", dest="grad_wire", choices=("fp32", "bf16"), default="fp32",
+                    help="DP gradient all-reduce dtype of the headline step (fp32 = parity)")
+    ap.add_argument("--dry-run", dest="dry_run", action="store_true",
+                    help="launcher / DP plumbing check on CPU over gloo (no GPU, no HIP): "
+                         "rank-0 broadcast + the bucketed gradient all-reduce, C1 model")
     return ap.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` outside torch.distributed.run: start N
+    ranks (one per GPU) through torch.distributed.run as a CHILD process and
+    exit with its code.  This parent never initialises HIP (no torch.cuda
+    call before or after), so the children own the GPUs; rank 0 prints the
+    JSON line on the shared stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, rank, world):
+    """Launcher / DP plumbing on CPU (gloo): the C1 model (BASELINE configs[0]
+    shapes: 2+2 layers d128) built with a rank-dependent seed, the Trainer's
+    rank-0 broadcast, then K timed exchange steps of the real GradBucketer
+    (per-layer async SUM all-reduce in backward order) over a rank-dependent
+    gradient.  No HIP kernel runs; the line says so (`dry_run`)."""
+    from smer_music_generation_amd.model import ScoreTransformer
+    from smer_music_generation_amd.train import GradBucketer, Trainer
+    from smer_music_generation_amd.vocab import WordVocab
+    dev = torch.device("cpu")
+    v = WordVocab(0, CTRL)
+    torch.manual_seed(100 + rank)  # deliberately different per rank
+    m = ScoreTransformer(309, 128, 4, 2, 2, 2048, 2400, 0.0, 0.0)
+    tr = Trainer(m, v, grad_wire_dtype=torch.bfloat16 if args.grad_wire == "bf16" else None)
+    in_sync = params_in_sync(m, dev, world)
+    grad = m.flat_grad()
+    bk = GradBucketer(grad, tr._ranges, wire_dtype=tr.grad_wire_dtype)
+    order = ["head"] + ["dec%d" % i for i in reversed(range(2))] + \
+        ["enc%d" % i for i in reversed(range(2))] + ["embedding"]
+
+    def step():
+        grad.fill_(float(rank + 1))
+        for name in order:
+            bk.reduce(name)
+        bk.finish()
+        return grad
+
+    dt, g = timed_steps(step, args.steps, args.warmup, dev, world)
+    dt = max_over_ranks(dt, dev, world)
+    want = world * (world + 1) / 2
+    return {"seconds": dt, "params_in_sync_at_init": in_sync,
+            "allreduce_ok": bool(torch.all(g == want).item()),
+            "bytes_per_step": grad.numel() * (2 if args.grad_wire == "bf16" else 4)}
 
 
 def data_feed(per_gpu_tokens_per_s, seconds=3.0):
@@ -426,10 +523,35 @@ def data_feed(per_gpu_tokens_per_s, seconds=3.0):
 
 def main():
     args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("bench: --gpus %d but WORLD_SIZE=%d; reporting the real world size"
+              % (args.gpus, world), file=sys.stderr)
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        r = dry_run(args, rank, world)
+        if rank == 0:
+            print(json.dumps({
+                "metric": "launcher dry run (DP plumbing on CPU, no GPU work; not a measurement)",
+                "value": None, "unit": "s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(1000 * r["seconds"] / args.steps, 3),
+                "higher_is_better": False, "scaling": "weak", "vs_baseline": None,
+                "dtype": args.grad_wire, "data": "synthetic", "dry_run": True,
+                "config": {"workload": "C1 model, rank-0 broadcast + bucketed gradient "
+                                       "all-reduce (gloo)", "parallelism": "dp%d" % world},
+                "params_in_sync_at_init": r["params_in_sync_at_init"],
+                "allreduce_ok": r["allreduce_ok"], "bytes_per_step": r["bytes_per_step"]}))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -437,7 +559,16 @@ def main():
     from smer_music_generation_amd import _lib
     _lib.load()
 
-    tr = bench_train(args, dev, rank, world)
+    wire = torch.bfloat16 if args.grad_wire == "bf16" else None
+    tr = bench_train(args, dev, rank, world, grad_wire=wire)
+    # DP only: the same step with the opt-in bf16 gradient all-reduce
+    # (half the xGMI bytes), reported beside the fp32 (parity) headline
+    tr_alt = None
+    if world > 1 and wire is None:
+        import copy
+        a = copy.copy(args)
+        a.roofline = False
+        tr_alt = bench_train(a, dev, rank, world, grad_wire=torch.bfloat16)
     c4 = bench_train_c4(args, dev, rank, world, "fp8") if args.c4 else None
     c4b = bench_train_c4(args, dev, rank, world, "bf16") if args.c4 else None
     inf = None
@@ -490,6 +621,11 @@ def main():
                        "tgt_len": args.tgt, "parallelism": "dp%d" % world},
             "train": {k: (round(val, 4) if isinstance(val, float) else val)
                       for k, val in tr.items() if k != "gemm"},
+            "train_bf16_allreduce": tr_alt and {
+                "tokens_per_s": round(tr_alt["tokens_per_s"], 1),
+                "ms_per_step": round(tr_alt["ms_per_step"], 3),
+                "note": "same step, DP gradient all-reduce in bf16 (opt-in; fp32 is the parity "
+                        "default)"},
             "roofline": roof,
             "infill": inf and {"metric": "infill tokens/s (greedy, KV-cached, batched; warm "
                                          "decode session)",

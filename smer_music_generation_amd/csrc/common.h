@@ -327,7 +327,12 @@ __device__ __forceinline__ uint2 smer_q8x8(const float (&v)[8], float qs) {
   for (int h = 0; h < 2; ++h) {
     float f[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) f[k] = fminf(fmaxf(v[4 * h + k] * qs, -448.f), 448.f);
+    for (int k = 0; k < 4; ++k) {
+      // saturate finite values to +-448; NaN passes through to the cast
+      // (fmaxf would turn it into -448: a diverged activation must stay NaN)
+      const float x = v[4 * h + k] * qs;
+      f[k] = x == x ? fminf(fmaxf(x, -448.f), 448.f) : x;
+    }
     int p = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
     p = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], p, true);
     w[h] = (uint32_t)p;
@@ -335,9 +340,11 @@ __device__ __forceinline__ uint2 smer_q8x8(const float (&v)[8], float qs) {
   return make_uint2(w[0], w[1]);
 }
 __device__ __forceinline__ float smer_absmax8(const float (&v)[8]) {
+  // NaN maps to +inf (fmaxf would drop it): the amax slot then reports the
+  // non-finite activation (Fp8Forward.finite) and the next scale falls back to 1
   float m = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(v[k]));
+  for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k] == v[k] ? fabsf(v[k]) : __builtin_inff());
   return m;
 }
 // wave-wide max, then at most one atomic per wave (every lane must call).

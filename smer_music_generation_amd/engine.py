@@ -315,7 +315,7 @@ class Engine:
                 from .fp8 import Fp8Forward
                 self._fp8 = Fp8Forward(self, dev)
             f8 = self._fp8
-            f8.begin(W)
+            f8.begin(W, training=training)
         x = torch.empty(B * S, d, dtype=dt, device=dev)
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
         xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)

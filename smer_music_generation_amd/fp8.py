@@ -41,18 +41,34 @@ class Fp8Forward:
         self.inv = torch.ones(N_SITES, device=device)
         self.t = 0
         self.cur = self.amax[1]
+        # amax sink of eval / no-grad forwards: written, never turned into scales
+        self._eval_amax = torch.zeros(N_SITES, dtype=torch.int32, device=device)
+        self.trained = False
         self._wkey = None
         self._w = {}
         self._wbuf = {}       # name -> (e4m3 buffer, inv view), persistent
         self._seg = None      # (key, device seg table, amax workspace, inv)
 
-    def begin(self, W=None):
+    def begin(self, W=None, training=True):
         """Start a forward: this forward's scales from the previous one's
-        amax; after a weight update, re-quantise every fp8 weight of W."""
-        prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
-        ops.fp8_scales(prev, self.qs, self.inv, nxt)
-        self.cur = nxt
-        self.t += 1
+        amax; after a weight update, re-quantise every fp8 weight of W.
+        Once a training forward has run, only training forwards advance the
+        scale history: an eval / no-grad forward (validation) reuses the
+        current scales and records its amax into a sink that never feeds a
+        scale.  Before the first training forward (an inference-only model)
+        every forward advances it, which calibrates the scales.
+        A non-finite activation makes its site's amax +inf (the producers map
+        NaN to inf in the amax and pass NaN through the e4m3 cast), so
+        `finite()` turns false after a diverged forward."""
+        calibrate = training or not self.trained
+        self.trained = self.trained or training
+        if calibrate:
+            prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
+            ops.fp8_scales(prev, self.qs, self.inv, nxt)
+            self.cur = nxt
+            self.t += 1
+        else:
+            self.cur = self._eval_amax
         if W is not None and self.eng._wgen != self._wkey:
             self._quantize_weights(W)
 
@@ -89,6 +105,12 @@ class Fp8Forward:
         ops.fp8_quantize_segments(seg, amax_ws, inv)
         self._w = {n: (self._wbuf[n], inv[k:k + 1]) for k, (n, _) in enumerate(ws)}
         self._wkey = self.eng._wgen
+
+    def finite(self):
+        """Device bool: every amax of the last training forward is finite
+        (the bits of +inf / NaN sort above every finite float)."""
+        last = self.amax[self.t % 2]
+        return (last < 0x7F800000).all()
 
     def site(self, name):
         i = self.sites.get(name)

@@ -57,7 +57,12 @@ def weighted_sampling(probs):
     # the reference's builtin sum() adds left to right from 0: the last
     # element of the (sequential) cumulative sum is that number exactly, in
     # 1/12 of the time; probs[argsort] holds np.sort's values (ties are
-    # equal values), so one sort serves both
+    # equal values), so one sort serves both.  `probs` is float64 here
+    # (sampling() widens the logits before the softmax), so builtin sum()
+    # adds float64 scalars under NumPy 1.x and 2.x alike: no promotion-rule
+    # dependence; a float32 input is rejected rather than silently diverging
+    if probs.dtype != np.float64:
+        raise TypeError("weighted_sampling expects float64 probabilities")
     probs /= np.add.accumulate(probs)[-1]
     sorted_index = np.argsort(probs)[::-1]
     return np.random.choice(sorted_index, size=1, p=probs[sorted_index])[0]
@@ -427,16 +432,38 @@ infill = generation_all
 _BATCH_SESSIONS = {}
 
 
-def _batch_session(model, R, Smax, Tmax, precision):
+def clear_decode_sessions(model=None):
+    """Drop the warm decode sessions of `model` (all models when None),
+    releasing their KV caches and captured graphs; the next
+    generation_batch call builds a fresh session."""
+    for key in [k for k, s in _BATCH_SESSIONS.items() if model is None or s.model is model]:
+        del _BATCH_SESSIONS[key]
+
+
+def _batch_session(model, R, Smax, Tmax, precision, exact_tmax=False, warm=True):
+    """A decode session for this call.  A cached one is reused only when it
+    still addresses the model's current weight buffers (moving the model
+    re-flattens them) and, for an explicit max_tgt, has exactly that
+    capacity (so the 'prefix exceeds max_tgt' error depends on this call's
+    arguments alone; the auto-sized capacity 100 * n_masks + 8 can never be
+    exceeded).  Before reuse the working weights are re-synchronised with the
+    fp32 master in place (a load_state_dict or an optimizer step since the
+    last call), so prefill and the captured step read current weights."""
     if precision is not None:
         model.set_precision(precision)
+    if not warm:
+        return DecodeSession(model, R, Smax, Tmax)
     key = (id(model), model.precision, R)
     s = _BATCH_SESSIONS.get(key)
     fits = (s is not None and s.model is model and s.Smax >= Smax and s.Tmax >= Tmax + 1
+            and (s.Tmax == Tmax + 1 or not exact_tmax)
             and (s.Smax >= 512) == (Smax >= 512) and (s.Tmax >= 512) == (Tmax + 1 >= 512))
     if fits:
-        s.src_len[:] = 0
-        return s
+        W = s.eng.weights(s.dt)  # re-casts in place when the master moved
+        if W.fc_w.data_ptr() == s.W.fc_w.data_ptr() and W.emb.data_ptr() == s.W.emb.data_ptr():
+            s.W = W
+            s.src_len[:] = 0
+            return s
     s = DecodeSession(model, R, Smax, Tmax)
     _BATCH_SESSIONS.pop(key, None)
     while len(_BATCH_SESSIONS) >= 2:
@@ -446,7 +473,8 @@ def _batch_session(model, R, Smax, Tmax, precision):
 
 
 def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logger=None,
-                     max_tgt=None, precision=None, return_stats=False, device_grammar=True):
+                     max_tgt=None, precision=None, return_stats=False, device_grammar=True,
+                     warm=True):
     """Decode many infill requests in lockstep on one KV-cached session.
 
     requests: list of (events, tracks_to_generate, bars_to_generate).
@@ -457,6 +485,9 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     which rebuild exactly the reference's event lists (and log the
     reference's redraw failures).  `device_grammar=False` (or sampling)
     keeps the per-step host loop.
+    warm: reuse (and keep) this model's cached decode session, as a serving
+    process would; False builds a private session freed after the call
+    (see also clear_decode_sessions).
     Returns a list of (restored, mask_track_names, mask_bar_names) (None
     where nothing was masked), and optionally {'tokens', 'steps'}."""
     t0 = time.perf_counter()
@@ -468,7 +499,8 @@ def generation_batch(model, requests, vocab, all_controls, *, greedy=True, logge
     model.eval()
     tokens = steps = 0
     with torch.no_grad():
-        sess = _batch_session(model, R, Smax, Tmax, precision)
+        sess = _batch_session(model, R, Smax, Tmax, precision, exact_tmax=max_tgt is not None,
+                              warm=warm)
         t1 = time.perf_counter()
         sess.prefill(list(range(R)), [p[0] for p in preps])
         torch.cuda.synchronize()

@@ -104,6 +104,10 @@ class _FakeDist:
         t.mul_(2.0)
         return _FakeWork() if async_op else None
 
+    def broadcast(self, t, src=0, group=None, async_op=False):
+        self.log.append(("broadcast", t.numel()))  # identical ranks: a no-op
+        return _FakeWork() if async_op else None
+
     def is_available(self):
         return True
 
@@ -134,6 +138,9 @@ def test_trainer_reduces_denominator_before_fused_ce(monkeypatch):
     monkeypatch.setattr(T.ops, "wce_fwd_bwd", wce)
     tr = T.Trainer(m2, v)
     assert tr.world == 2
+    # the flat parameters are broadcast from rank 0 at init, once
+    assert log == [("broadcast", m2.flat_parameters().numel())], log
+    log.clear()
     loss2 = tr.step(bt)
     torch.cuda.synchronize()
     assert log[0] == ("all_reduce", 1) and log[1] == ("wce", 0), log[:3]
