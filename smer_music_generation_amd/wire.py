@@ -227,10 +227,30 @@ def change_controls(original_event, controls):
                         ev[a] = ev[a + 1] = ev[a + 2] = 'unk'
 
     # copy each bar's tensile to the bar end and each track's 3 controls to
-    # the track end, walking backwards so earlier positions stay valid
-    marks = sorted([i for i, t in enumerate(ev) if t in set(names)] + bars)
+    # the track end: one forward pass that rebuilds the list (O(n)); the
+    # reference's backward walk of list inserts (O(n^2)) is kept only for an
+    # event list whose bars do not each hold exactly n_tracks track tokens
+    nameset = set(names)
+    marks = sorted([i for i, t in enumerate(ev) if t in nameset] + bars)
     marks.append(len(ev))
     barset = set(bars)
+    bar_idx = [k for k, p in enumerate(marks[:-1]) if p in barset]
+    regular = all(k + n_tracks + 1 < len(marks) and
+                  not any(marks[k + t] in barset for t in range(1, n_tracks + 1)) and
+                  (k + n_tracks + 1 == len(marks) - 1 or marks[k + n_tracks + 1] in barset)
+                  for k in bar_idx)
+    if regular:
+        out = ev[:marks[0]]
+        for k in bar_idx:
+            bar_pos = marks[k]
+            out += ev[bar_pos:marks[k + 1]]
+            for t in range(n_tracks):
+                a, b = marks[k + t + 1], marks[k + t + 2]
+                out += ev[a:b]
+                out += ev[a + 1:a + N_TRACK_CONTROLS + 1]
+            out.append(ev[bar_pos + 1])
+        ev[:] = out
+        return ev
     for bp in range(len(marks) - 1, -1, -1):
         if marks[bp] not in barset:
             continue

@@ -156,6 +156,40 @@ def test_gemm256_streamed_epilogue_gate(M, N, K, bk):
     assert rel_err(C, base + G.float()) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K,bk", [(32768, 2048, 512, True), (16384, 1536, 256, True),
+                                      (16384, 512, 2048, False), (65536, 768, 768, True),
+                                      (8192, 2304, 1536, False), (65536, 256, 256, False)])
+def test_gemm_ring_matches_256_kernel(M, N, K, bk, monkeypatch):
+    """The ring kernel (LDS-DMA ring across tiles, accumulator epilogue with
+    deferred stores) against the two-stage 256x256 kernel on whole-tile
+    shapes: 1-4 tiles per workgroup, K = 256 (half the deferred groups
+    flushed at the tile end) to 2048, every epilogue form the step uses.
+    The k order of the accumulation is the same, so outputs are compared
+    bit for bit, plus against fp32."""
+    O = ops()
+    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    Wm = W if bk else W.t().contiguous()
+    bias = torch.randn(N, device=dev)
+    R = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    cases = [dict(bias=bias, relu=True, drop_p=0.1, seed=3), dict(bias=bias, residual=R, drop_p=0.1, seed=5),
+             dict(gate=R, gate_scale=1.25), dict()]
+    base = None
+    for kw in cases:
+        outs = []
+        for ring in ("1", "0"):
+            monkeypatch.setenv("SMER_GEMM_RING", ring)
+            C = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+            O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)
+            outs.append(C)
+        torch.cuda.synchronize()
+        assert not torch.isnan(outs[0]).any(), kw.keys()
+        assert torch.equal(outs[0], outs[1]), (kw.keys(), (outs[0].float() - outs[1].float()).abs().max().item())
+        if not kw:
+            base = A.float() @ W.float().t()
+            assert rel_err(outs[0], base) < 1e-2
+
+
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128

@@ -362,9 +362,9 @@ def test_warm_session_after_load_state_dict_matches_fresh(golden_dir, precision)
     old = run()
     sess = next(iter(G._BATCH_SESSIONS.values()))
     g = torch.Generator().manual_seed(5)
+    sd_cpu = {k: t.detach().cpu() for k, t in m.state_dict().items()}
     sd2 = {k: (t + 0.5 * torch.randn(t.shape, generator=g) * t.std() if t.dim() > 1 and k != "pos_enc.pe"
-               else t).clone() for k, t in m.state_dict().items()}
-    sd2 = {k: t.cpu() for k, t in sd2.items()}
+               else t).clone() for k, t in sd_cpu.items()}
     m.load_state_dict(sd2)
     warm = run()
     assert next(iter(G._BATCH_SESSIONS.values())) is sess  # really the warm session

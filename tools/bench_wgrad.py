@@ -30,4 +30,6 @@ for (Mo, Nin, T) in ((512, 512, 8192), (2048, 512, 8192), (512, 2048, 8192), (15
     dw = torch.zeros(Mo, Nin, device="cuda")
     db = torch.zeros(Mo, device="cuda")
     t = timeit(lambda: ops.linear_wgrad(dy, x, dw, db=db))
-    print("wgrad M%-5d N%-5d K%-6d %8.1f us %7.1f TF" % (Mo, Nin, T, t, 2 * Mo * Nin * T / t / 1e6))
+    tb = timeit(lambda: torch.matmul(dy.t(), x))  # hipBLASLt reference point (no bias grad)
+    print("wgrad M%-5d N%-5d K%-6d %8.1f us %7.1f TF   [torch/hipBLASLt %8.1f us %7.1f TF]"
+          % (Mo, Nin, T, t, 2 * Mo * Nin * T / t / 1e6, tb, 2 * Mo * Nin * T / tb / 1e6), flush=True)
