@@ -227,7 +227,11 @@ def bench_infill(args, dev, rank):
     tw = time.perf_counter()
     _, wst = generation_batch(m, warm, v, all_controls, greedy=True, return_stats=True)
     torch.cuda.synchronize()
-    cold = wst["tokens"] / (time.perf_counter() - tw)
+    cold_s = time.perf_counter() - tw
+    cold = wst["tokens"] / cold_s
+    cold_phases = dict({k: round(wst[k], 4) for k in ("prepare_s", "prefill_s", "decode_s", "step_call_s")},
+                       **{k: round(v, 4) for k, v in wst.get("decode_phases_s", {}).items()},
+                       total_s=round(cold_s, 4))
     reqs = _infill_requests(args.infill_batch, args.seq, 100 * rank)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -236,6 +240,7 @@ def bench_infill(args, dev, rank):
     dt = time.perf_counter() - t0
     src_len = float(np.mean([len(r[0]) for r in reqs]))
     return {"tokens": st["tokens"], "steps": st["steps"], "seconds": dt, "cold_tokens_per_s": cold,
+            "cold_phases_s": cold_phases,
             "phases_s": dict({k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s",
                                                            "step_call_s")},
                              **{k: round(v, 4) for k, v in st.get("decode_phases_s", {}).items()}),
@@ -255,7 +260,14 @@ def bench_infill_batch1(args, dev, rank):
     ac = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
     (wev, wtr, wbr), = _infill_requests(1, args.seq, 8100 + rank)
     np.random.seed(1)
-    generation_all(m, list(wev), dev, v, None, ac, wtr, wbr)  # warm-up (graph capture)
+    # the process's first plugin call (session + graph capture): its latency
+    # is the cold batch-1 figure
+    torch.cuda.synchronize()
+    tc = time.perf_counter()
+    cst = {}
+    generation_all(m, list(wev), dev, v, None, ac, wtr, wbr, stats=cst)
+    torch.cuda.synchronize()
+    cold_s = time.perf_counter() - tc
     reqs = _infill_requests(8, args.seq, 8000 + 100 * rank)
     from smer_music_generation_amd.generation import _prepare
     src_len = float(np.mean([len(_prepare(list(ev), v, tr, br)[0]) for ev, tr, br in reqs]))
@@ -270,7 +282,9 @@ def bench_infill_batch1(args, dev, rank):
     dt = time.perf_counter() - t0
     return {"value": round(steps / dt, 1), "tokens": steps, "seconds": round(dt, 4),
             "requests": len(reqs), "mean_src_len": round(src_len, 1),
-            "ms_per_token": round(1000 * dt / max(1, steps), 3)}
+            "ms_per_token": round(1000 * dt / max(1, steps), 3),
+            "cold_call_s": round(cold_s, 4), "cold_call_tokens": cst.get("steps"),
+            "warm_call_s_mean": round(dt / len(reqs), 4)}
 
 
 def bench_infill_c5(args, dev, rank):
@@ -636,7 +650,8 @@ def main():
                                "decode_steps": inf["steps"], "tokens": inf["tokens"],
                                "ms_per_decode_step": round(inf["ms_per_decode_step"], 3),
                                "roofline": inf["roofline"],
-                               "phases_s": inf["phases_s"], "parallelism": "replicas",
+                               "phases_s": inf["phases_s"], "cold_phases_s": inf["cold_phases_s"],
+                               "parallelism": "replicas",
                                "batch1": b1 and dict(b1, metric="plugin call generation_all "
                                                      "(batch 1, default weighted sampling, "
                                                      "KV-cached), tokens/s")},

@@ -261,16 +261,6 @@ __device__ __forceinline__ void lds_wait() {
   else if constexpr (N == 15) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
   else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8 || N == 15, "add the count");
 }
-// lgkmcnt(n) for an n that folds to a constant after unrolling (0..15)
-#define SMER_LGW(n) case n: asm volatile("s_waitcnt lgkmcnt(" #n ")" ::: "memory"); break;
-__device__ __forceinline__ void lds_wait_dyn(int n) {
-  switch (n) {
-    SMER_LGW(0) SMER_LGW(1) SMER_LGW(2) SMER_LGW(3) SMER_LGW(4) SMER_LGW(5) SMER_LGW(6) SMER_LGW(7)
-    SMER_LGW(8) SMER_LGW(9) SMER_LGW(10) SMER_LGW(11) SMER_LGW(12) SMER_LGW(13) SMER_LGW(14)
-    default: asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory"); break;
-  }
-}
-#undef SMER_LGW
 // Retire only the asm reads of one fragment set, issued before CNT younger
 // (compiler-visible) LDS reads whose waits hipcc places itself.
 template <int CNT, int NB>

@@ -1237,338 +1237,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
-// Ring GEMM: the forward (NT) and dgrad (NN) shapes on 256x256 tiles, built
-// around two measured costs of gemm256_bf16_kernel at K = 512 (FFN1 of C2:
-// 90 us, of which 26 us vanish without the stores and 17 us without the
-// MFMAs): every tile paid its prologue load latency and its epilogue (four
-// LDS passes, eight barriers, a store burst the next tile's first
-// vmcnt(0) then waited for) in series with its main loop.
-//  * K is staged in 32-deep slots (A 16 KiB + B 16 KiB) through a ring of
-//    four LDS slots filled by LDS-DMA three slots ahead.  The ring runs over
-//    the whole persistent work list, so the next tile's first slots land
-//    while this tile finishes; waits are counted (s_waitcnt vmcnt(n) for the
-//    exact number of younger VMEM instructions), one barrier per slot.
-//  * MFMA operands swapped (C^T = B A^T): a lane then owns 4 consecutive
-//    output columns of one row per 16x16 block, so the epilogue runs on the
-//    accumulators in place (bias, ReLU, dropout, residual / gate) and packs
-//    each group to 8 bytes of bf16.  Those 32 groups per lane are NOT stored
-//    at once: they stay in 64 registers and two go out per slot of the next
-//    tile (16 slots), so the chip's output writes are spread over the next
-//    tile's MFMAs instead of arriving as one burst per tile.
-//  * Per slot the 12 fragment reads (B first) are retired one A fragment at
-//    a time (lgkmcnt(7 - i)), so the first MFMAs start behind 5 reads.
-// Whole tiles only: M, N % 256 == 0, K % 256 == 0, bf16 C (host: ring_ok).
-// ---------------------------------------------------------------------------
-namespace {
-constexpr int RK = 32;                  // K depth of one ring slot
-constexpr int R_OP = G2 * RK * 2;       // 16 KiB per operand per slot
-constexpr int R_SLOT = 2 * R_OP;        // 32 KiB
-constexpr int R_LDS = 4 * R_SLOT + 2 * 1024;  // 4 slots + two tiles' bias rows
-
-// row image of a slot: row r at r * 64 B, its four 16-B k-chunks XOR
-// ring_swz(r): the 16 lanes of every ds_read_b128 lane group (gfx950 LDS
-// table) then hit 16 distinct 16-B slots of the 256-B bank row
-__device__ __forceinline__ int ring_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
-
-// Per-thread byte offsets of a slot's two 1-KiB LDS-DMA pieces (the lane
-// part of the source address; constant for the whole kernel): KC, 16 rows x
-// 64 B per piece; column image (as g2_glds), 2 k-rows x 512 B per piece.
-template <bool KC>
-__device__ __forceinline__ void ring_voffs(int (&vo)[2], long ld, int lane, int wave) {
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int chunk = wave * 2 + c;
-    if (KC) {
-      const int row = chunk * 16 + (lane >> 2);
-      const int lc = (lane & 3) ^ ring_swz(row);
-      vo[c] = (int)(((long)row * ld + lc * 8) * 2);
-    } else {
-      const int k = chunk * 2 + (lane >> 5);
-      const int lc = (lane & 31) ^ (2 * (int)col_swz(k));
-      vo[c] = (int)(((long)k * ld + lc * 8) * 2);
-    }
-  }
-}
-// one operand slot (16 KiB) by buffer LDS-DMA: uniform byte offset `soff`
-// of the slot's first row (KC: row r0, k0; column image: k-row k0, col r0)
-__device__ __forceinline__ void ring_glds(char* slot, __amdgpu_buffer_rsrc_t rsrc, const int (&vo)[2], int soff,
-                                          int wave) {
-  typedef __attribute__((address_space(3))) void lvoid;
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lvoid*)(slot + (wave * 2 + c) * 1024), 16, vo[c], soff, 0, 0);
-}
-
-// fragment of 16 rows from rbase (multiple of 16) x the slot's 32 k (asm
-// reads: retired by the caller's counted lgkmcnt waits)
-__device__ __forceinline__ bf16x8 ring_frag_row(const char* slot, int rbase, int lane) {
-  const int c16 = lane & 15, g = lane >> 4;
-  return __builtin_bit_cast(bf16x8, lds_read_b128_async(slot, (rbase + c16) * 64 + ((g ^ ring_swz(c16)) << 4)));
-}
-__device__ __forceinline__ bf16x8 ring_frag_col(const char* slot, int rbase, int lane) {
-  const int g = lane >> 4, c16 = lane & 15, q = c16 >> 2, p = c16 & 3;
-  const int u = (rbase >> 2) + p;
-  const int k0 = 8 * g + q, k1 = k0 + 4;
-  const bf16x4 lo = lds_read_tr16_async(slot, k0 * 512 + ((u ^ (4 * col_swz(k0))) << 3));
-  const bf16x4 hi = lds_read_tr16_async(slot, k1 * 512 + ((u ^ (4 * col_swz(k1))) << 3));
-  return cat4(lo, hi);
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n.  n = the VMEM
-// instructions this wave issued after the one waited for; n above 31 waits
-// as for 31 (longer, never shorter).
-#define SMER_VMW(n) case n: __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x0F70); break;
-__device__ __forceinline__ void vm_wait_dyn(int n) {
-  switch (n < 31 ? n : 31) {
-    SMER_VMW(0) SMER_VMW(1) SMER_VMW(2) SMER_VMW(3) SMER_VMW(4) SMER_VMW(5) SMER_VMW(6) SMER_VMW(7)
-    SMER_VMW(8) SMER_VMW(9) SMER_VMW(10) SMER_VMW(11) SMER_VMW(12) SMER_VMW(13) SMER_VMW(14)
-    SMER_VMW(15) SMER_VMW(16) SMER_VMW(17) SMER_VMW(18) SMER_VMW(19) SMER_VMW(20) SMER_VMW(21)
-    SMER_VMW(22) SMER_VMW(23) SMER_VMW(24) SMER_VMW(25) SMER_VMW(26) SMER_VMW(27) SMER_VMW(28)
-    SMER_VMW(29) SMER_VMW(30)
-    default: __builtin_amdgcn_s_waitcnt((31 & 15) | ((31 >> 4) << 14) | 0x0F70); break;
-  }
-}
-#undef SMER_VMW
-
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  bf16x2_t v;
-  v[0] = (bf16)a;
-  v[1] = (bf16)b;
-  return __builtin_bit_cast(uint32_t, v);
-}
-__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
-}  // namespace
-
-template <bool BKC>
-__global__ __launch_bounds__(512, 1) void gemm_ring_kernel(int M, int N, int K,
-                                                           const bf16* __restrict__ A, long lda,
-                                                           const bf16* __restrict__ B, long ldb,
-                                                           GemmEpi e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  // wave index made provably uniform (readfirstlane): every address term
-  // built from it stays scalar
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int nbm = M / G2, nbn = N / G2, nwg = nbm * nbn;
-  // persistent XCD-aware work list (as gemm256_bf16_kernel)
-  const int braw = blockIdx.x, xcd = braw & 7;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int xcount = q8 + (xcd < r8 ? 1 : 0);
-  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
-  const int jfirst = braw >> 3;
-  const int ntl = jfirst < xcount ? (xcount - jfirst + pstride - 1) / pstride : 0;
-  constexpr int GM = 4;
-  auto tile_of = [&](int t, int& m0, int& n0) {
-    const int wgid = xstart + jfirst + t * pstride;
-    const int grp = wgid / (GM * nbn);
-    const int first_m = grp * GM;
-    const int gsz = min(nbm - first_m, GM);
-    const int within = wgid % (GM * nbn);
-    m0 = (first_m + within % gsz) * G2;
-    n0 = (within / gsz) * G2;
-  };
-  const int nks = K / RK;  // slots per tile, a multiple of 8
-  const int total = ntl * nks;
-  char* const bias_lds = smem + 4 * R_SLOT;
-  typedef __attribute__((address_space(3))) void lvoid;
-  // buffer descriptors (32-bit byte offsets: the host checks the extents)
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, -1, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)B, (short)0, -1, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rBias = __builtin_amdgcn_make_buffer_rsrc((void*)e.bias, (short)0, -1, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(e.C, (short)0, -1, 0x00020000);
-  const void* xsrc = e.residual ? e.residual : e.gate;
-  const long ldx = e.residual ? e.ldr : e.ldg;
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc((void*)xsrc, (short)0, -1, 0x00020000);
-  int voA[2], voB[2];
-  ring_voffs<true>(voA, lda, lane, wave);
-  ring_voffs<BKC>(voB, ldb, lane, wave);
-
-  // VMEM instructions issued by this thread so far (wave-uniform), and the
-  // count right after the DMA of each of the next three slots (mk0 = slot p's)
-  int issued = 0;
-  auto issue = [&](int q) {
-    if (q >= total) return;
-    const int t = q / nks, kk = q - t * nks;
-    int m0, n0;
-    tile_of(t, m0, n0);
-    char* slot = smem + (q & 3) * R_SLOT;
-    ring_glds(slot, rA, voA, (int)(((long)m0 * lda + kk * RK) * 2), wave);
-    ring_glds(slot + R_OP, rB, voB,
-              BKC ? (int)(((long)n0 * ldb + kk * RK) * 2) : (int)(((long)kk * RK * ldb + n0) * 2), wave);
-    issued += 4;
-    if (kk == 0 && e.bias) {
-      // the tile's bias row for its epilogue (every wave loads the same
-      // 1 KiB: each one's own vmcnt wait then covers the bytes it reads)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rBias, (lvoid*)(bias_lds + (t & 1) * 1024), 16, lane * 16,
-                                               n0 * 4, 0, 0);
-      issued += 1;
-    }
-  };
-  issue(0);
-  int mk0 = issued;
-  issue(1);
-  int mk1 = issued;
-  issue(2);
-  int mk2 = issued;
-
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-  u32x2 out[32];  // the previous tile's packed bf16 output, (i, j) = (g >> 2, g & 3)
-  int pm0 = 0, pn0 = 0;
-  const long ldc = e.ldc;
-  const int vo_c = (int)(((long)c16 * ldc + 4 * g) * 2);  // lane part of a C / X group address
-  const int vo_x = (int)(((long)c16 * ldx + 4 * g) * 2);
-  auto store_group = [&](int gi) {  // gi compile-time after unrolling / in a switch arm
-    const int i = gi >> 2, j = gi & 3;
-    const int soff = (int)((((long)pm0 + wm * 128 + i * 16) * ldc + pn0 + wn * 64 + j * 16) * 2);
-    __builtin_amdgcn_raw_buffer_store_b64(out[gi], rC, vo_c, soff, 0);
-  };
-
-  for (int t = 0; t < ntl; ++t) {
-    int m0, n0;
-    tile_of(t, m0, n0);
-    f32x4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll 1
-    for (int kk = 0; kk < nks; ++kk) {
-      const int p = t * nks + kk;
-      vm_wait_dyn(issued - mk0);  // my DMA of slot p has landed
-      __builtin_amdgcn_s_barrier();  // everyone's; slot p - 1 fully read
-      __builtin_amdgcn_sched_barrier(0);
-      issue(p + 3);
-      const int mk3 = issued;
-      // two of the previous tile's 32 output groups per slot (a switch keeps
-      // every register index static)
-      if (t > 0 && kk < 16) {
-        switch (kk) {
-#define SMER_SG2(n) case n: store_group(2 * (n)); store_group(2 * (n) + 1); break;
-          SMER_SG2(0) SMER_SG2(1) SMER_SG2(2) SMER_SG2(3) SMER_SG2(4) SMER_SG2(5) SMER_SG2(6) SMER_SG2(7)
-          SMER_SG2(8) SMER_SG2(9) SMER_SG2(10) SMER_SG2(11) SMER_SG2(12) SMER_SG2(13) SMER_SG2(14)
-          default: store_group(30); store_group(31); break;
-#undef SMER_SG2
-        }
-        issued += 2;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const char* slot = smem + (p & 3) * R_SLOT;
-      bf16x8 bfr[4], af[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bfr[j] = BKC ? ring_frag_row(slot + R_OP, wn * 64 + j * 16, lane)
-                     : ring_frag_col(slot + R_OP, wn * 64 + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = ring_frag_row(slot, wm * 128 + i * 16, lane);
-      // a rolling window of four A fragments: A[i + 4] is requested right
-      // behind the MFMAs of A[i] (into its registers)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        lds_wait_dyn(7 - i < 3 ? 7 - i : 3);  // B and A[0..i] landed (LDS returns in order)
-        if (i == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(bfr[j]));
-        }
-        asm volatile("" : "+v"(af[i]));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-        if (i + 4 < 8) af[i + 4] = ring_frag_row(slot, wm * 128 + (i + 4) * 16, lane);
-      }
-      mk0 = mk1;
-      mk1 = mk2;
-      mk2 = mk3;
-    }
-
-    // ---- epilogue of tile t: the groups of tile t - 1 not yet stored go
-    // out now (K = 256: 16 slots carried only half of them), then the
-    // accumulators become the new packed output
-    if (t > 0 && nks < 16) {
-#pragma unroll
-      for (int gi = 16; gi < 32; ++gi) store_group(gi);
-      issued += 16;
-    }
-    if (xsrc) {  // residual / gate rows into the output registers
-#pragma unroll
-      for (int gi = 0; gi < 32; ++gi) {
-        const int i = gi >> 2, j = gi & 3;
-        const int soff = (int)((((long)m0 + wm * 128 + i * 16) * ldx + n0 + wn * 64 + j * 16) * 2);
-        out[gi] = __builtin_amdgcn_raw_buffer_load_b64(rX, vo_x, soff, 0);
-      }
-      issued += 32;
-    }
-    float bv[4][4];
-    if (e.bias) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint4 w = lds_read_b128_async(bias_lds + (t & 1) * 1024, (wn * 64 + j * 16 + 4 * g) * 4);
-        bv[j][0] = __uint_as_float(w.x); bv[j][1] = __uint_as_float(w.y);
-        bv[j][2] = __uint_as_float(w.z); bv[j][3] = __uint_as_float(w.w);
-      }
-      lds_wait<0>();
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(bv[j][r]));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[j][r] = 0.f;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = m0 + wm * 128 + i * 16 + c16;
-      const uint32_t rkey = e.drop_thr ? smer_rowkey(e.seed, (uint32_t)row) : 0u;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int gi = i * 4 + j;
-        const int col = n0 + wn * 64 + j * 16 + 4 * g;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * e.alpha + bv[j][r];
-        if (e.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (e.drop_thr) {
-          const uint32_t h0 = smer_pair_bits(rkey, (uint32_t)col >> 1);
-          const uint32_t h1 = smer_pair_bits(rkey, ((uint32_t)col >> 1) + 1);
-          v[0] = (h0 & 0xFFFFu) >= e.drop_thr ? v[0] * e.drop_scale : 0.f;
-          v[1] = (h0 >> 16) >= e.drop_thr ? v[1] * e.drop_scale : 0.f;
-          v[2] = (h1 & 0xFFFFu) >= e.drop_thr ? v[2] * e.drop_scale : 0.f;
-          v[3] = (h1 >> 16) >= e.drop_thr ? v[3] * e.drop_scale : 0.f;
-        }
-        if (xsrc) {
-          const float x[4] = {bf16_lo(out[gi].x), bf16_hi(out[gi].x), bf16_lo(out[gi].y), bf16_hi(out[gi].y)};
-          if (e.residual) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += x[r];
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = x[r] > 0.f ? v[r] * e.gate_scale : 0.f;
-          }
-        }
-        out[gi] = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-      }
-    }
-    pm0 = m0;
-    pn0 = n0;
-  }
-  if (ntl > 0) {  // the last tile's output
-#pragma unroll
-    for (int gi = 0; gi < 32; ++gi) store_group(gi);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
 // Split-K (deterministic slabs) for a pure Cf (+)= A.B^T epilogue with few
 // output tiles and a long K, i.e. the weight gradients (K = tokens): without
 // it a [512 x 1536] wgrad occupies 48 of 256 CUs.
@@ -1584,18 +1252,7 @@ static bool smer_gemm_glds_enabled() {
 
 // SMER_GEMM256=0 keeps every shape on the 128x128 kernel (A/B, tests).
 static bool smer_gemm256_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SMER_GEMM256");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// SMER_GEMM_RING=0 keeps whole-tile forward / dgrad shapes on the 256x256
-// two-stage kernel (A/B, tests)
-static bool smer_gemm_ring_enabled() {
-  const char* e = getenv("SMER_GEMM_RING");  // read per call: tests flip it in-process
+  const char* e = getenv("SMER_GEMM256");  // read per call: A/B scripts flip it in-process
   return !(e && e[0] == '0');
 }
 
@@ -1715,23 +1372,6 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                          (const bf16*)A, lda, (const bf16*)B, ldb, e);
     return;
   }
-  // whole-tile forward / dgrad with a bf16 output: the ring kernel
-  if (AK && !rowsum && smer_gemm_ring_enabled() && M % G2 == 0 && N % G2 == 0 && K % 256 == 0 &&
-      e.vec && e.C && !e.Cf && !e.kv && !e.q8 && !(e.residual && e.gate)) {
-    const long t2 = (long)(M / G2) * (N / G2);
-    if (t2 >= smer_num_cus()) {
-      const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
-      static bool attr_set = false;
-      if (!attr_set) {
-        hipFuncSetAttribute((const void*)gemm_ring_kernel<BKC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            R_LDS);
-        attr_set = true;
-      }
-      hipLaunchKernelGGL(gemm_ring_kernel<BKC>, dim3(grid), dim3(512), R_LDS, s, M, N, K, (const bf16*)A, lda,
-                         (const bf16*)B, ldb, e);
-      return;
-    }
-  }
   // large-M forward / dgrad: 256x256 tiles when they fill the chip
   if (AK && !rowsum && K % G2K == 0 && smer_gemm256_enabled()) {
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
@@ -1824,9 +1464,86 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                        (const float*)rs_part, rowsum, e.rs_accumulate);
   }
 }
+// Skinny f32 NT GEMM (parity-mode decode steps: M = 2 rows per request).
+// The 64x64 tile kernel runs N / 64 workgroups there (8 for a d = 512
+// Linear), each re-reading a 64-row weight strip: the batch-1 fp32 decode
+// step took 3.2 ms.  Here a workgroup owns 16 output columns x up to 16
+// rows; its 4 waves split K, lane (c16, kq) streams W[col][k + 4 kq .. + 3]
+// with 16-B loads (the 16 columns x 16 k of a wave step: 1 KiB), four
+// k-steps in flight.  Partial dot products reduced over kq by shuffles and
+// over the waves through LDS in fixed order (deterministic).
+constexpr int SKF_BN = 16, SKF_BM = 16, SKF_NW = 4, SKF_UNR = 4;
+__global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_f32_kernel(int M, int N, int K,
+                                                                      const float* __restrict__ A, long lda,
+                                                                      const float* __restrict__ B, long ldb,
+                                                                      GemmEpi e) {
+  __shared__ float red[SKF_NW][SKF_BM][SKF_BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, kq = lane >> 4;
+  const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
+  const int col = n0 + c16;
+  const bool colok = col < N;
+  const int mrows = min(SKF_BM, M - m0);
+  const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  float acc[SKF_BM];
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) acc[r] = 0.f;
+  const int nsteps = (K + 15) / 16;  // 16 k per wave step (4 lanes x 4)
+  for (int s0 = wave; s0 < nsteps; s0 += SKF_NW * SKF_UNR) {
+    float4 b[SKF_UNR];
+#pragma unroll
+    for (int u = 0; u < SKF_UNR; ++u) {
+      const int k = (s0 + u * SKF_NW) * 16;
+      b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < SKF_UNR; ++u) {
+      const int k = (s0 + u * SKF_NW) * 16 + 4 * kq;
+      if (k >= K) continue;
+#pragma unroll
+      for (int r = 0; r < SKF_BM; ++r) {
+        if (r < mrows) {
+          const float4 a = *reinterpret_cast<const float4*>(A + (long)(m0 + r) * lda + k);
+          acc[r] = fmaf(a.x, b[u].x, acc[r]);
+          acc[r] = fmaf(a.y, b[u].y, acc[r]);
+          acc[r] = fmaf(a.z, b[u].z, acc[r]);
+          acc[r] = fmaf(a.w, b[u].w, acc[r]);
+        }
+      }
+    }
+  }
+  // sum the four kq lane groups (lanes c16, +16, +32, +48), then the waves
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) {
+    acc[r] += __shfl_xor(acc[r], 16, 64);
+    acc[r] += __shfl_xor(acc[r], 32, 64);
+  }
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < SKF_BM; ++r) red[wave][r][c16] = acc[r];
+  }
+  __syncthreads();
+  if (tid < SKF_BM * SKF_BN) {
+    const int r = tid / SKF_BN, c = tid % SKF_BN;
+    if (r < mrows && n0 + c < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < SKF_NW; ++w) t += red[w][r][c];
+      epi_apply<float>(e, M, N, m0 + r, n0 + c, t);
+    }
+  }
+}
+
 template <bool AK, bool BKC>
 static void launch_f32(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                        const GemmEpi& e, hipStream_t s) {
+  if (AK && BKC && M <= 64 && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+      (((uintptr_t)A | (uintptr_t)B) & 15) == 0) {
+    const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+    hipLaunchKernelGGL(gemm_skinny_f32_kernel, grid, dim3(64 * SKF_NW), 0, s, M, N, K, (const float*)A,
+                       lda, (const float*)B, ldb, e);
+    return;
+  }
   dim3 grid((N + 63) / 64, (M + 63) / 64);
   hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC>), grid, dim3(256), 0, s, M, N, K,
                      (const float*)A, lda, (const float*)B, ldb, e);

@@ -194,7 +194,8 @@ static int ln_fwd_rpw(int M) {
 // where 4x the column partials cost more than the extra parallelism gives)
 constexpr int LN_BWD_ROWS = 64;
 constexpr int LN_BWD_ROWS_SMALL = 16;
-static inline int ln_bwd_rows(int M) { return M <= 16384 ? LN_BWD_ROWS_SMALL : LN_BWD_ROWS; }
+static inline int ln_bwd_rows_fixed(int M) { return M <= 16384 ? LN_BWD_ROWS_SMALL : LN_BWD_ROWS; }
+static int ln_bwd_rows(int M, int N);  // below the kernel (needs its occupancy)
 
 // One wave per row, NC 16-B chunks per lane (N <= 512 * NC); a wave takes
 // its 16 rows of the block RB at a time with all RB rows' loads issued
@@ -579,8 +580,37 @@ extern "C" int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, floa
   return SMER_OK;
 }
 
+// Rows per workgroup.  N > 512 at large M (C4: 65536 x 768): 64-row blocks
+// made 1024 workgroups for ~768 resident slots (3 per CU at that register
+// footprint), so a second, one-third-full round of workgroups ran alone
+// (134.7 us, 3.0 TB/s).  There the rows are spread over exactly the resident
+// slots (a multiple of 16 rows per workgroup: every wave's batches whole),
+// one round.  N <= 512 keeps the measured 64 (C2: 4.8 TB/s).
+static int ln_bwd_rows(int M, int N) {
+  const int fixed = ln_bwd_rows_fixed(M);
+  const char* e = getenv("SMER_LN_BWD_BALANCE");
+  if (M <= 16384 || N <= 512 || (e && e[0] == '0')) return fixed;
+  static int occ[2] = {0, 0};  // NC = 2, NC = 4
+  const int which = N <= 1024 ? 0 : 1;
+  if (!occ[which]) {
+    int nb = 0;
+    const void* kern = which == 0 ? (const void*)ln_bwd_kernel<bf16, false, 2, 2, true>
+                                  : (const void*)ln_bwd_kernel<bf16, false, 4, 1, true>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 1;
+    occ[which] = nb;
+  }
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const long resident = (long)cus * occ[which];
+  const long per = (M + resident - 1) / resident;
+  const int rows = (int)((per + 15) / 16 * 16);
+  return rows > fixed ? fixed : rows;  // never more rows (fewer blocks) than the fixed split
+}
+
 extern "C" size_t smer_layernorm_bwd_workspace(int M, int N) {
-  size_t nblk = (size_t)(M + ln_bwd_rows(M) - 1) / ln_bwd_rows(M);
+  size_t nblk = (size_t)(M + ln_bwd_rows(M, N) - 1) / ln_bwd_rows(M, N);
   return nblk * 2 * N * sizeof(float) + smer_col_reduce_scratch((int)nblk, 2 * N);
 }
 
@@ -598,7 +628,7 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
                "smer_layernorm_bwd: workspace too small");
   if (M == 0) return SMER_OK;
   hipStream_t s = (hipStream_t)stream;
-  const int rpb = ln_bwd_rows(M);
+  const int rpb = ln_bwd_rows(M, N);
   int nblk = (M + rpb - 1) / rpb;
   uint32_t thr = smer_drop_thr16(drop_p);
   float ds = smer_drop_scale16(thr);
@@ -671,7 +701,7 @@ extern "C" int smer_layernorm_param_reduce(int M, int N, void* workspace, size_t
   SMER_REQUIRE(workspace && ws_bytes >= smer_layernorm_bwd_workspace(M, N),
                "smer_layernorm_param_reduce: workspace too small");
   if (M == 0 || (!dgamma && !dbeta)) return SMER_OK;
-  const int nblk = (M + ln_bwd_rows(M) - 1) / ln_bwd_rows(M);
+  const int nblk = (M + ln_bwd_rows(M, N) - 1) / ln_bwd_rows(M, N);
   float* part = (float*)workspace;
   hipStream_t s = (hipStream_t)stream;
   if (dgamma && dbeta)

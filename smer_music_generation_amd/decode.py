@@ -33,6 +33,23 @@ import torch
 from . import ops
 
 
+def _capture(stream, fn):
+    """Capture fn()'s launches on `stream` into a HIP graph.  Not the
+    torch.cuda.graph context manager: its __enter__ empties the caching
+    allocator (hipFree of every cached segment -- 40-140 ms after a training
+    step had filled the cache, the whole cold-call capture cost in the
+    round-3 bench), which a decode step allocating a few small buffers in
+    the graph's private pool does not need."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(stream):
+        g.capture_begin()
+        try:
+            fn()
+        finally:
+            g.capture_end()
+    return g
+
+
 class DecodeSession:
     def __init__(self, model, max_requests, max_src, max_tgt, precision=None, use_graph=True):
         if precision is not None:
@@ -262,12 +279,8 @@ class DecodeSession:
         torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                self._run()
+        self.graph = _capture(s, self._run)
         torch.cuda.current_stream().wait_stream(s)
-        self.graph = g
 
     def _load_feeds(self, feeds):
         """Host-built step rows: feeds = [(slot, new_token_ids (1 or 2),
@@ -352,11 +365,7 @@ class DecodeSession:
         t_b = time.perf_counter()
         gs = torch.cuda.Stream()
         gs.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(gs):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=gs):
-                self._run()
-                grammar()
+        g = _capture(gs, lambda: (self._run(), grammar()))
         torch.cuda.current_stream().wait_stream(gs)
         torch.cuda.synchronize()
         t_c = time.perf_counter()

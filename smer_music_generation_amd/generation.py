@@ -12,6 +12,9 @@ Differences, all opt-in keywords with reference defaults:
     `DecodeSession` (one encoder pass per request) instead of re-running the
     full model per token; `use_kv_cache=False` is the reference algorithm.
   * `greedy=False`: True replaces `weighted_sampling` by argmax.
+  * `generation_all(..., precision="fp32")`: the plugin call decodes in
+    fp32 whatever precision the model trains in (bit-exact ids); None
+    decodes at the model's own precision.
   * `generation_batch(...)`: many requests decoded in lockstep.
 The grammar state machine, the -100 logit masking, the float64 softmax and
 the numpy RNG consumption are the reference's, so with the same
@@ -380,12 +383,47 @@ def _prepare(events, vocab, tracks_to_generate, bars_to_generate):
     return src, mtn, mbn, target, no_whole
 
 
+class _Precision:
+    """Run a block at another arithmetic precision of the model, restoring
+    the model's own afterwards (the plugin call decodes in fp32 whatever
+    precision the model trains in)."""
+
+    def __init__(self, model, precision):
+        self.model, self.want = model, precision
+        self.prev = None
+
+    def __enter__(self):
+        if self.want is not None and self.want != self.model.precision:
+            self.prev = self.model.precision
+            self.model.set_precision(self.want)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            self.model.set_precision(self.prev)
+        return False
+
+
 def generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
-                   bars_to_generate, *, greedy=False, use_kv_cache=True, stats=None):
+                   bars_to_generate, *, greedy=False, use_kv_cache=True, stats=None,
+                   precision="fp32"):
     """`generation.py:468-696`.  Returns (restored '<U9' tokens,
     mask_track_names, mask_bar_names) or None (nothing masked / on error,
     after printing it, as the reference does).  `stats` (a dict, opt-in)
-    receives the number of decode steps (= tokens drawn)."""
+    receives the number of decode steps (= tokens drawn).
+    precision: arithmetic of this call's decode.  "fp32" (default) gives
+    the reference's token ids bit for bit (north_star: bit-exact greedy ids;
+    sampled ids are the same draws of the same numpy stream) whatever
+    precision the model trains in; None decodes at the model's own precision
+    (bf16 for a default-constructed model: faster, ids may differ at
+    near-ties); the batched serving API `generation_batch` keeps None."""
+    with _Precision(model, precision):
+        return _generation_all(model, events, device, vocab, logger, all_controls,
+                               tracks_to_generate, bars_to_generate, greedy, use_kv_cache, stats)
+
+
+def _generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
+                    bars_to_generate, greedy, use_kv_cache, stats):
     try:
         src, mtn, mbn, target, no_whole = _prepare(events, vocab, tracks_to_generate,
                                                    bars_to_generate)

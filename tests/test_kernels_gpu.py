@@ -156,40 +156,6 @@ def test_gemm256_streamed_epilogue_gate(M, N, K, bk):
     assert rel_err(C, base + G.float()) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K,bk", [(32768, 2048, 512, True), (16384, 1536, 256, True),
-                                      (16384, 512, 2048, False), (65536, 768, 768, True),
-                                      (8192, 2304, 1536, False), (65536, 256, 256, False)])
-def test_gemm_ring_matches_256_kernel(M, N, K, bk, monkeypatch):
-    """The ring kernel (LDS-DMA ring across tiles, accumulator epilogue with
-    deferred stores) against the two-stage 256x256 kernel on whole-tile
-    shapes: 1-4 tiles per workgroup, K = 256 (half the deferred groups
-    flushed at the tile end) to 2048, every epilogue form the step uses.
-    The k order of the accumulation is the same, so outputs are compared
-    bit for bit, plus against fp32."""
-    O = ops()
-    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
-    Wm = W if bk else W.t().contiguous()
-    bias = torch.randn(N, device=dev)
-    R = torch.randn(M, N, device=dev).to(torch.bfloat16)
-    cases = [dict(bias=bias, relu=True, drop_p=0.1, seed=3), dict(bias=bias, residual=R, drop_p=0.1, seed=5),
-             dict(gate=R, gate_scale=1.25), dict()]
-    base = None
-    for kw in cases:
-        outs = []
-        for ring in ("1", "0"):
-            monkeypatch.setenv("SMER_GEMM_RING", ring)
-            C = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
-            O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)
-            outs.append(C)
-        torch.cuda.synchronize()
-        assert not torch.isnan(outs[0]).any(), kw.keys()
-        assert torch.equal(outs[0], outs[1]), (kw.keys(), (outs[0].float() - outs[1].float()).abs().max().item())
-        if not kw:
-            base = A.float() @ W.float().t()
-            assert rel_err(outs[0], base) < 1e-2
-
-
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128
@@ -853,6 +819,39 @@ def test_gemm64_mid_size_epilogues(M, N, K, bk):
     ref = torch.where(R.float() > 0, base * 1.5, torch.zeros_like(base))
     torch.cuda.synchronize()
     assert rel_err(C, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,N", [(65536, 768), (20000, 1024), (40000, 2048)])
+def test_layernorm_bwd_balanced_grid(M, N, monkeypatch):
+    """LayerNorm backward at large M and N > 512 spreads the rows over the
+    resident workgroup slots (one round): dx bit-identical to the fixed
+    64-row split, dgamma / dbeta equal up to the partials' summation order,
+    and both against fp32 torch."""
+    O = ops()
+    x = (torch.randn(M, N, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    g = torch.randn(N, device=dev)
+    b = torch.randn(N, device=dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    O.layernorm(x, g, b, y, mean, rstd)
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    res = {}
+    for bal in ("1", "0"):
+        monkeypatch.setenv("SMER_LN_BWD_BALANCE", bal)
+        dx = torch.empty_like(x)
+        dg = torch.zeros(N, device=dev)
+        db = torch.zeros(N, device=dev)
+        O.layernorm_bwd(dy, x, mean, rstd, g, dx, dgamma=dg, dbeta=db)
+        res[bal] = (dx, dg, db)
+    torch.cuda.synchronize()
+    assert torch.equal(res["1"][0], res["0"][0])
+    assert rel_err(res["1"][1], res["0"][1]) < 1e-5 and rel_err(res["1"][2], res["0"][2]) < 1e-5
+    xf = x.float().requires_grad_(True)
+    gf, bf = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xf, (N,), gf, bf, 1e-5).backward(dy.float())
+    assert rel_err(res["1"][0], xf.grad) < 2e-2
+    assert rel_err(res["1"][1], gf.grad) < 1e-2 and rel_err(res["1"][2], bf.grad) < 1e-2
 
 
 def test_layernorm_fwd_rows_kernel_bit_identical_to_one_row_kernel(tmp_path):

@@ -212,7 +212,8 @@ def test_generation_batch_matches_single(golden_dir, precision):
             for r in g["cases"] if r["mode"] == "greedy"]
     batch = generation_batch(m, reqs, v, g["all_controls"], greedy=True)
     for (ev, tr, br), got in zip(reqs, batch):
-        single = generation_all(m, list(ev), dev, v, None, g["all_controls"], tr, br, greedy=True)
+        single = generation_all(m, list(ev), dev, v, None, g["all_controls"], tr, br, greedy=True,
+                                precision=None)  # the model's own precision, as the batch
         assert [str(x) for x in got[0]] == [str(x) for x in single[0]]
     if precision == "fp32":
         for rec, got in zip([r for r in g["cases"] if r["mode"] == "greedy"], batch):
