@@ -1163,12 +1163,19 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
     long row_stride, long req_stride, long head_stride, const int32_t* __restrict__ row_req,
     const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale,
-    DecQ dq = DecQ{}) {
+    DecQ dq = DecQ{}, int odd_first = 0) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int GPW = 64 / LPK;  // key groups per wave
   constexpr int KPB = NW * GPW;  // keys per block step
   __shared__ float red_m[NW][LPK], red_l[NW][LPK], red_a[NW][LPK][VEC];
-  const int h = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;  // heads of a row dispatch together
+  // heads of a row dispatch together.  odd_first: block rows y < n/2 take
+  // the odd rows (a decode session's last-token slots, the live ones), the
+  // rest the even rows (mostly one-key dummies): dispatched in row order the
+  // live blocks of an XCD alternated with dummies and so landed on every
+  // other CU of its round-robin
+  const int ny = gridDim.y, yb = blockIdx.y;
+  const int r = (odd_first && !(ny & 1)) ? (yb < (ny >> 1) ? 2 * yb + 1 : 2 * (yb - (ny >> 1))) : yb;
+  const int h = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int sub = lane % LPK, grp = wave * GPW + lane / LPK;
   const int nk = row_nkeys[r];
@@ -1559,6 +1566,12 @@ extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
   return SMER_OK;
 }
 
+// SMER_DECODE_ODD_FIRST=0: blocks in plain row order (A/B)
+static int smer_dec_odd_first() {
+  const char* e = getenv("SMER_DECODE_ODD_FIRST");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, long ldy,
                                     const float* gamma, const float* beta, float eps, const void* wq,
                                     long ldw, const float* bq, void* x_out, long ldx, int dmodel,
@@ -1579,6 +1592,7 @@ extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, lon
   if (n_rows == 0) return SMER_OK;
   if (head_stride <= 0) head_stride = D;
   DecQ dq{(const bf16*)y, ldy, gamma, beta, eps, (const bf16*)wq, ldw, bq, (bf16*)x_out, ldx, dmodel};
+  const int odd = smer_dec_odd_first();
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(H, n_rows);
   // long memories (>= 2048 key rows of capacity): next key step's loads
@@ -1589,7 +1603,7 @@ extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, lon
 #define SMER_DEC_QLN(P, DM)                                                                        \
   hipLaunchKernelGGL((attn_decode_vec_kernel<bf16, 8, 4, 8, P, DM>), grid, dim3(512), 0, s,        \
                      (const bf16*)nullptr, 0L, (const bf16*)kcache, (const bf16*)vcache, row_stride, \
-                     req_stride, head_stride, row_req, row_nkeys, (bf16*)o, ldo, scale, dq)
+                     req_stride, head_stride, row_req, row_nkeys, (bf16*)o, ldo, scale, dq, odd)
   if (pipe) {
     if (dmodel == 512) SMER_DEC_QLN(true, 512);
     else if (dmodel == 768) SMER_DEC_QLN(true, 768);
@@ -1627,19 +1641,20 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
     const long cap_rows = head_stride != D ? head_stride / (row_stride > 0 ? row_stride : 1)
                                            : req_stride / (row_stride > 0 ? row_stride : 1);
     const bool big = cap_rows >= 512, pipe = cap_rows >= 2048;
+    const int odd = smer_dec_odd_first();
 #define SMER_DEC_VEC(T, L)                                                                        \
   if (pipe)                                                                                       \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8, true>), grid, dim3(512), 0, s,         \
                        (const T*)q, ldq, (const T*)kcache, (const T*)vcache, row_stride,          \
-                       req_stride, head_stride, row_req, row_nkeys, (T*)o, ldo, scale);           \
+                       req_stride, head_stride, row_req, row_nkeys, (T*)o, ldo, scale, DecQ{}, odd); \
   else if (big)                                                                                   \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 4, 8>), grid, dim3(512), 0, s, (const T*)q,  \
                        ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride,            \
-                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale);                       \
+                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale, DecQ{}, odd);          \
   else                                                                                            \
     hipLaunchKernelGGL((attn_decode_vec_kernel<T, L, 2, 4>), grid, dim3(256), 0, s, (const T*)q,  \
                        ldq, (const T*)kcache, (const T*)vcache, row_stride, req_stride,            \
-                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale)
+                       head_stride, row_req, row_nkeys, (T*)o, ldo, scale, DecQ{}, odd)
     if (ok && (lpk == 4 || lpk == 8 || lpk == 16)) {
       if (dtype == SMER_BF16) {
         if (lpk == 4) SMER_DEC_VEC(bf16, 4); else if (lpk == 8) SMER_DEC_VEC(bf16, 8); else SMER_DEC_VEC(bf16, 16);
