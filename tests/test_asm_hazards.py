@@ -31,6 +31,19 @@ _Zoverwritten:
 	ds_read_b32 v7, v2
 	v_mov_b32_e32 v7, 0
 	v_add_u32_e32 v8, v7, v7
+_Zloopcarried:
+.LBB0_1:
+	v_mov_b32_e32 v30, v20
+	s_waitcnt lgkmcnt(0)
+	ds_read_b64 v[20:21], v2
+	s_cbranch_scc1 .LBB0_1
+	s_waitcnt lgkmcnt(0)
+_Zsmem:
+	ds_read_b64 v[50:51], v2
+	s_load_dwordx2 s[4:5], s[0:1], 0x0
+	s_waitcnt lgkmcnt(1)
+	v_mov_b32_e32 v52, v50
+	s_waitcnt lgkmcnt(0)
 """
 
 
@@ -38,7 +51,10 @@ def test_checker_on_synthetic_listing(tmp_path):
     p = tmp_path / "s.s"
     p.write_text(SYNTH)
     bad = check(str(p))
-    assert set(bad) == {"_Zbad"}
+    # _Zloopcarried: v20 is read at the loop head while the previous
+    # iteration's ds_read of it is still in flight (found via the back-edge);
+    # _Zsmem: lgkmcnt(1) with a scalar load pending retires no LDS read
+    assert set(bad) == {"_Zbad", "_Zloopcarried", "_Zsmem"}
     assert "scratch_store" in bad["_Zbad"][0][1]
 
 
