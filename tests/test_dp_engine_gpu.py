@@ -178,4 +178,7 @@ def test_two_ranks_gloo_engine_matches_single_process(tmp_path):
         got = torch.load(os.path.join(tmp_path, "rank%d.pt" % rk), weights_only=True)
         assert abs(float(got["loss"]) - loss.item()) < 1e-5 * max(1.0, loss.item())
         err = float((got["grad"] - g).norm() / g.norm())
-        assert err < 1e-5, (rk, err)
+        # fp32 summation order differs: a rank's decoder Linears have M = 64
+        # rows and run the skinny fp32 kernel (K split over 4 waves), the
+        # single process's M = 128 the tile kernel; measured 1.0e-5
+        assert err < 5e-5, (rk, err)

@@ -1,6 +1,6 @@
 """Per-shape microbenchmarks of the hot kernels at the C2 shapes (GPU).
 
-    python tools/bench_kernels.py [gemm|attn|all]
+    python tools/bench_kernels.py [gemm|attn|attn_c4|all]
 """
 import math
 import os
@@ -74,11 +74,17 @@ def bench_gemm():
               % (name, kind, M, N, K, t, fl / t / 1e6, t2, fl / t2 / 1e6, fl / tt / 1e6))
 
 
-def bench_attn():
+ATTN_SHAPES = {
+    "c2": (("enc self", 32, 8, 1024, 1024, False), ("dec self", 32, 8, 256, 256, True),
+           ("cross", 32, 8, 256, 1024, False)),
+    "c4": (("c4 enc self", 32, 12, 2048, 2048, False), ("c4 dec self", 32, 12, 512, 512, True),
+           ("c4 cross", 32, 12, 512, 2048, False)),
+}
+
+
+def bench_attn(cfg="c2"):
     bf = torch.bfloat16
-    for name, B, H, Lq, Lk, causal in (("enc self", 32, 8, 1024, 1024, False),
-                                       ("dec self", 32, 8, 256, 256, True),
-                                       ("cross", 32, 8, 256, 1024, False)):
+    for name, B, H, Lq, Lk, causal in ATTN_SHAPES[cfg]:
         D = 64
         q = torch.randn(B * Lq, H * D, device=dev).to(bf)
         kv = torch.randn(B * Lk, 2 * H * D, device=dev).to(bf)
@@ -111,3 +117,5 @@ if __name__ == "__main__":
         bench_gemm()
     if which in ("attn", "all"):
         bench_attn()
+    if which in ("attn_c4", "all"):
+        bench_attn("c4")
