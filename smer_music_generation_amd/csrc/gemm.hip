@@ -1289,15 +1289,18 @@ static int smer_splitk_depth() {
   return v;
 }
 
-// SMER_WGRAD256=1 moves the weight gradients to the 256x256 kernel (A/B);
+// Weight gradients on the 256x256 kernel: for outputs of at least 768 x 768
+// (C4: 90.1 vs 91.1 ms per step; at C2's 512-wide outputs the 128x128
+// kernel with its smaller split-K slabs is as fast or faster).
+// SMER_WGRAD256=1 / 0 forces it on / off for every shape (A/B);
 // SMER_WGRAD256_DEPTH: minimum K depth of its split-K slices
-static bool smer_wgrad256_enabled() {
+static bool smer_wgrad256_enabled(int M, int N) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD256");
-    v = (e && e[0] == '1') ? 1 : 0;
+    v = (e && e[0] == '1') ? 1 : (e && e[0] == '0') ? 0 : 2;
   }
-  return v == 1;
+  return v == 1 || (v == 2 && (long)M * N >= 768L * 768);
 }
 static int smer_wgrad256_depth() {
   static int v = -1;
@@ -1327,6 +1330,31 @@ static long smer_skinny16_cap() {  // workgroups per CU (SMER_SKINNY16_CAP; A/B 
   return v;
 }
 
+// Resident split-K workgroups per 2 CUs (SMER_WGRAD_WGP2: 4 = two per CU,
+// the default; 2 = one per CU; 1 = one per two CUs).  The weight gradients
+// run on a second stream beside the main chain: a smaller persistent grid
+// leaves CUs (and LDS) to the main stream's kernels and cuts the split-K
+// slab bytes in proportion.
+static long smer_wgrad_resident() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD_WGP2");
+    v = e ? std::max(1, std::min(4, atoi(e))) : 4;
+  }
+  return std::max(8L, (v * (long)smer_num_cus()) / 2);
+}
+
+// fewest 256x256 tiles for which a forward / dgrad shape takes the 256x256
+// kernel (SMER_G256_MIN, A/B runs; default: one per CU)
+static long smer_g256_min_tiles() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_G256_MIN");
+    v = e ? std::max(1, atoi(e)) : smer_num_cus();
+  }
+  return v;
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -1335,7 +1363,7 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   // ~2 resident workgroups per CU, K slices >= 1024 deep: more slices only
   // add slab traffic (split * M * N * 8 bytes through HBM)
   // (floor: a partial second wave of workgroups costs a whole slice time)
-  long s = (2L * smer_num_cus()) / tiles;
+  long s = smer_wgrad_resident() / tiles;
   s = std::min<long>(s, K / smer_splitk_depth());
   // slabs of M*N floats plus M floats of row-sum partials per K slice
   s = std::min<long>(s, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
@@ -1375,7 +1403,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   // large-M forward / dgrad: 256x256 tiles when they fill the chip
   if (AK && !rowsum && K % G2K == 0 && smer_gemm256_enabled()) {
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
-    if (t2 >= smer_num_cus()) {
+    if (t2 >= smer_g256_min_tiles()) {
       const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
       static bool attr_set = false;  // > 64 KiB dynamic LDS must be opted into
       if (!attr_set) {
@@ -1397,7 +1425,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   }
   // weight gradients (both operands column images, pure fp32 output): the
   // 256x256 tile when its split-K fills the chip with >= 512-deep slices
-  if (!AK && !BKC && K % G2K == 0 && ws && smer_wgrad256_enabled()) {
+  if (!AK && !BKC && K % G2K == 0 && ws && smer_wgrad256_enabled(M, N)) {
     const bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr &&
                          ((long)M * N) % 4 == 0;
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
@@ -1447,9 +1475,10 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     split = (K + kchunk - 1) / kchunk;
   }
   float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
-  // persistent grid: two resident workgroups per CU (LDS 64 KiB, <= 256 VGPRs)
+  // persistent grid: two resident workgroups per CU (LDS 64 KiB, <= 256 VGPRs);
+  // split-K weight gradients: smer_wgrad_resident()
   const long nwg = (long)tiles * split;
-  const long resident = 2L * smer_num_cus();
+  const long resident = split > 1 ? smer_wgrad_resident() : 2L * smer_num_cus();
   const int grid = nwg > resident ? (int)(resident & ~7L) : (int)nwg;
   // LDS-DMA staging needs whole 64-deep K steps in every slice
   const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled();

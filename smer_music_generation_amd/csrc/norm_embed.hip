@@ -580,6 +580,181 @@ extern "C" int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, floa
   return SMER_OK;
 }
 
+// bf16 backward for 512 < N <= 768 (C4: d = 768): lane l owns columns
+// 8l .. 8l+7 (16-B chunk) and 512 + 4l .. +3 (8-B chunk), so every lane
+// carries 12 columns instead of ln_bwd_kernel's two 16-B chunks with half
+// the lanes idle on the second; RB rows per batch, the next batch fetched
+// raw before this batch's math.  Same per-element arithmetic, dropout
+// decisions (pair hashes of (row, col)) and partial layout as ln_bwd_kernel;
+// the row sums s1 / s2 add the lane's 12 columns in another order.
+template <int RB>
+__global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16* __restrict__ dy,
+                                                        long lddy, const bf16* __restrict__ x, long ldx,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd,
+                                                        const float* __restrict__ gamma,
+                                                        bf16* __restrict__ dx, long lddx,
+                                                        bf16* __restrict__ dxd, long ldxd,
+                                                        uint32_t thr, uint32_t seed, float dscale,
+                                                        float* __restrict__ part, int rows_per_blk) {
+  __shared__ float red[4][2][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = 8 * lane, ct = 512 + 4 * lane;
+  const bool tok = ct < N;
+  float gm[12], pg[12], pb[12];
+  {
+    const float4 a = *reinterpret_cast<const float4*>(gamma + c0);
+    const float4 b2 = *reinterpret_cast<const float4*>(gamma + c0 + 4);
+    const float4 t = tok ? *reinterpret_cast<const float4*>(gamma + ct) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gm[0] = a.x; gm[1] = a.y; gm[2] = a.z; gm[3] = a.w; gm[4] = b2.x; gm[5] = b2.y; gm[6] = b2.z;
+    gm[7] = b2.w; gm[8] = t.x; gm[9] = t.y; gm[10] = t.z; gm[11] = t.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  const int r0 = blockIdx.x * rows_per_blk;
+  uint4 px[RB], pd[RB];
+  uint2 pxt[RB], pdt[RB];
+  float pmu[RB], prs[RB];
+  auto fetch = [&](int rb) {
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = min(r0 + wave + 4 * (rb + u), M - 1);
+      pmu[u] = mean[row];
+      prs[u] = rstd[row];
+      px[u] = *reinterpret_cast<const uint4*>(x + (long)row * ldx + c0);
+      pd[u] = *reinterpret_cast<const uint4*>(dy + (long)row * lddy + c0);
+      if (tok) {
+        pxt[u] = *reinterpret_cast<const uint2*>(x + (long)row * ldx + ct);
+        pdt[u] = *reinterpret_cast<const uint2*>(dy + (long)row * lddy + ct);
+      } else {
+        pxt[u] = make_uint2(0u, 0u);
+        pdt[u] = make_uint2(0u, 0u);
+      }
+    }
+  };
+  fetch(0);
+  for (int rb = 0; rb < rows_per_blk / 4; rb += RB) {
+    float xh[RB][12], gd[RB][12], mu[RB], rs[RB];
+    bool ok[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = r0 + wave + 4 * (rb + u);
+      ok[u] = row < M;
+      mu[u] = ok[u] ? pmu[u] : 0.f;
+      rs[u] = ok[u] ? prs[u] : 0.f;
+      const bf16x8 xv = __builtin_bit_cast(bf16x8, px[u]);
+      const bf16x8 dv = __builtin_bit_cast(bf16x8, pd[u]);
+      const bf16x4 xt = __builtin_bit_cast(bf16x4, pxt[u]);
+      const bf16x4 dt = __builtin_bit_cast(bf16x4, pdt[u]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { xh[u][i] = (float)xv[i]; gd[u][i] = (float)dv[i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { xh[u][8 + i] = (float)xt[i]; gd[u][8 + i] = (float)dt[i]; }
+    }
+    if (rb + RB < rows_per_blk / 4) fetch(rb + RB);
+    float s1[RB], s2[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = 0.f;
+      s2[u] = 0.f;
+      if (ok[u])
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          if (i >= 8 && !tok) continue;
+          const float dv = gd[u][i];
+          const float h = (xh[u][i] - mu[u]) * rs[u];
+          const float gg = dv * gm[i];
+          xh[u][i] = h;
+          gd[u][i] = gg;
+          s1[u] += gg;
+          s2[u] += gg * h;
+          pg[i] += dv * h;
+          pb[i] += dv;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = wave_sum(s1[u]) / N;
+      s2[u] = wave_sum(s2[u]) / N;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      if (!ok[u]) continue;
+      const int row = r0 + wave + 4 * (rb + u);
+      float o[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) o[i] = rs[u] * (gd[u][i] - s1[u] - xh[u][i] * s2[u]);
+      bf16x8 w;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = (bf16)o[i];
+      *reinterpret_cast<bf16x8*>(dx + (long)row * lddx + c0) = w;
+      bf16x4 wt;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wt[i] = (bf16)o[8 + i];
+      if (tok) *reinterpret_cast<bf16x4*>(dx + (long)row * lddx + ct) = wt;
+      if (dxd) {
+        float od[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) od[i] = o[i];
+        const uint32_t rowkey = thr ? smer_rowkey(seed, (uint32_t)row) : 0u;
+        if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)c0, od);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = (bf16)od[i];
+        *reinterpret_cast<bf16x8*>(dxd + (long)row * ldxd + c0) = w;
+        if (tok) {
+          float ot[4] = {o[8], o[9], o[10], o[11]};
+          if (thr) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const uint32_t hh = smer_pair_bits(rowkey, ((uint32_t)ct >> 1) + k);
+              ot[2 * k] = (hh & 0xFFFFu) >= thr ? ot[2 * k] * dscale : 0.f;
+              ot[2 * k + 1] = (hh >> 16) >= thr ? ot[2 * k + 1] * dscale : 0.f;
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) wt[i] = (bf16)ot[i];
+          *reinterpret_cast<bf16x4*>(dxd + (long)row * ldxd + ct) = wt;
+        }
+      }
+    }
+  }
+  if (!part) return;
+  // the 4 waves' column partials in fixed order: columns 0..511 in two
+  // 256-column halves, then the tail
+  for (int base = 0; base < N; base += 256) {
+    if (base < 512) {
+      if (c0 >= base && c0 < base + 256)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          red[wave][0][c0 + i - base] = pg[i];
+          red[wave][1][c0 + i - base] = pb[i];
+        }
+    } else if (tok) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[wave][0][4 * lane + i] = pg[8 + i];
+        red[wave][1][4 * lane + i] = pb[8 + i];
+      }
+    }
+    __syncthreads();
+    const int col = threadIdx.x;
+    if (base + col < N) {
+      const float a = (red[0][0][col] + red[1][0][col]) + (red[2][0][col] + red[3][0][col]);
+      const float b = (red[0][1][col] + red[1][1][col]) + (red[2][1][col] + red[3][1][col]);
+      part[(long)blockIdx.x * 2 * N + base + col] = a;
+      part[(long)blockIdx.x * 2 * N + N + base + col] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// SMER_LN_BWD_T4=0 keeps 512 < N <= 768 on ln_bwd_kernel (A/B, tests)
+static bool ln_bwd_t4_enabled() {
+  const char* e = getenv("SMER_LN_BWD_T4");  // per call: tests flip it in-process
+  return !(e && e[0] == '0');
+}
+static inline bool ln_bwd_t4_shape(int N) { return N > 512 && N <= 768 && N % 4 == 0; }
+
 // Rows per workgroup.  N > 512 at large M (C4: 65536 x 768): 64-row blocks
 // made 1024 workgroups for ~768 resident slots (3 per CU at that register
 // footprint), so a second, one-third-full round of workgroups ran alone
@@ -590,12 +765,13 @@ static int ln_bwd_rows(int M, int N) {
   const int fixed = ln_bwd_rows_fixed(M);
   const char* e = getenv("SMER_LN_BWD_BALANCE");
   if (M <= 16384 || N <= 512 || (e && e[0] == '0')) return fixed;
-  static int occ[2] = {0, 0};  // NC = 2, NC = 4
-  const int which = N <= 1024 ? 0 : 1;
+  static int occ[3] = {0, 0, 0};  // NC = 2, NC = 4, t4
+  const int which = ln_bwd_t4_shape(N) && ln_bwd_t4_enabled() ? 2 : N <= 1024 ? 0 : 1;
   if (!occ[which]) {
     int nb = 0;
-    const void* kern = which == 0 ? (const void*)ln_bwd_kernel<bf16, false, 2, 2, true>
-                                  : (const void*)ln_bwd_kernel<bf16, false, 4, 1, true>;
+    const void* kern = which == 2   ? (const void*)ln_bwd_t4_kernel<4>
+                       : which == 0 ? (const void*)ln_bwd_kernel<bf16, false, 2, 2, true>
+                                    : (const void*)ln_bwd_kernel<bf16, false, 4, 1, true>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 1;
     occ[which] = nb;
   }
@@ -651,7 +827,13 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
     else if (N <= 1024) LNB1(T, F, 2, 2);          \
     else LNB1(T, F, 4, 1);                         \
   } while (0)
-  if (dtype == SMER_BF16) { if (dy_f32) LNB(bf16, true); else LNB(bf16, false); }
+  if (dtype == SMER_BF16 && !dy_f32 && ln_bwd_t4_shape(N) && ln_bwd_t4_enabled() &&
+      ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+      ((uintptr_t)dx_drop & 15) == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && ldxd % 8 == 0) {
+    hipLaunchKernelGGL((ln_bwd_t4_kernel<4>), dim3(nblk), dim3(256), 0, s, M, N, (const bf16*)dy, lddy,
+                       (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop, ldxd,
+                       thr, seed, ds, part, rpb);
+  } else if (dtype == SMER_BF16) { if (dy_f32) LNB(bf16, true); else LNB(bf16, false); }
   else if (dtype == SMER_F32) { LNB(float, false); }
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB

@@ -873,3 +873,39 @@ def test_layernorm_fwd_rows_kernel_bit_identical_to_one_row_kernel(tmp_path):
     for rpw in ("1", "2", "4"):
         for k in outs["0"].files:
             assert np.array_equal(outs["0"][k], outs[rpw][k]), (rpw, k)
+
+
+@pytest.mark.parametrize("M,N", [(65536, 768), (1000, 768), (16387, 640), (77, 520)])
+def test_layernorm_bwd_t4_kernel(M, N, monkeypatch):
+    """512 < N <= 768: the 12-columns-per-lane backward (ln_bwd_t4_kernel)
+    against the two-chunk ln_bwd_kernel (SMER_LN_BWD_T4=0) and fp32 torch:
+    the dropout copy zeroes exactly the same elements, dx agrees up to the
+    row sums' summation order, dgamma / dbeta up to the partials' order."""
+    O = ops()
+    x = (torch.randn(M, N, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    g = torch.randn(N, device=dev)
+    b = torch.randn(N, device=dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    O.layernorm(x, g, b, y, mean, rstd)
+    dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    res = {}
+    for t4 in ("1", "0"):
+        monkeypatch.setenv("SMER_LN_BWD_T4", t4)
+        dx = torch.empty_like(x)
+        dxd = torch.empty_like(x)
+        dg = torch.zeros(N, device=dev)
+        db = torch.zeros(N, device=dev)
+        O.layernorm_bwd(dy, x, mean, rstd, g, dx, dx_drop=dxd, drop_p=0.1, seed=7, dgamma=dg, dbeta=db)
+        res[t4] = (dx, dxd, dg, db)
+    torch.cuda.synchronize()
+    new, old = res["1"], res["0"]
+    assert torch.equal(new[1] == 0, old[1] == 0)
+    assert rel_err(new[0], old[0]) < 1e-2 and rel_err(new[1], old[1]) < 1e-2
+    assert rel_err(new[2], old[2]) < 1e-5 and rel_err(new[3], old[3]) < 1e-5
+    xf = x.float().requires_grad_(True)
+    gf, bf = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xf, (N,), gf, bf, 1e-5).backward(dy.float())
+    assert rel_err(new[0], xf.grad) < 2e-2
+    assert rel_err(new[2], gf.grad) < 1e-2 and rel_err(new[3], bf.grad) < 1e-2

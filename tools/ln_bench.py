@@ -1,4 +1,4 @@
-"""LayerNorm forward / backward timing at the C2 shapes (rows x 512)."""
+"""LayerNorm forward / backward timing at the C2 (rows x 512) and C4 (rows x 768) shapes."""
 import os
 import sys
 
@@ -22,8 +22,7 @@ def timeit(f, iters=20):
     return e0.elapsed_time(e1) * 1e3 / iters
 
 
-for M in (32768, 8192):
-    N = 512
+for M, N in ((32768, 512), (8192, 512), (65536, 768), (16384, 768)):
     x = torch.randn(M, N, device=dev).to(torch.bfloat16)
     g = torch.randn(N, device=dev)
     b = torch.randn(N, device=dev)
@@ -40,4 +39,4 @@ for M in (32768, 8192):
                                           dgamma=dg, dbeta=db))
     fb = 2 * M * N * 2 / tf / 1e3
     bb = 4 * M * N * 2 / tb / 1e3
-    print("M=%d fwd %.1f us (%.0f GB/s)  bwd %.1f us (%.0f GB/s)" % (M, tf, fb, tb, bb), flush=True)
+    print("M=%d N=%d fwd %.1f us (%.0f GB/s)  bwd %.1f us (%.0f GB/s)" % (M, N, tf, fb, tb, bb), flush=True)
