@@ -1289,9 +1289,12 @@ static int smer_splitk_depth() {
   return v;
 }
 
-// Weight gradients on the 256x256 kernel: for outputs of at least 768 x 768
-// (C4: 90.1 vs 91.1 ms per step; at C2's 512-wide outputs the 128x128
-// kernel with its smaller split-K slabs is as fast or faster).
+// Weight gradients on the 256x256 kernel for outputs of at least 1536 x 768
+// (tools/bench_wgrad.py c4: 3072x768x65536 350 vs 426 us, 768x3072 316 vs
+// 387, 2304x768 271 vs 315; 768x768 equal at K = 65536 and 54 vs 43 us at
+// 16384; C4 step 90.1 vs 91.1 ms with every wgrad on it).  At C2's
+// 512-wide outputs the 128x128 kernel with its smaller split-K slabs is as
+// fast or faster.
 // SMER_WGRAD256=1 / 0 forces it on / off for every shape (A/B);
 // SMER_WGRAD256_DEPTH: minimum K depth of its split-K slices
 static bool smer_wgrad256_enabled(int M, int N) {
@@ -1300,7 +1303,7 @@ static bool smer_wgrad256_enabled(int M, int N) {
     const char* e = getenv("SMER_WGRAD256");
     v = (e && e[0] == '1') ? 1 : (e && e[0] == '0') ? 0 : 2;
   }
-  return v == 1 || (v == 2 && (long)M * N >= 768L * 768);
+  return v == 1 || (v == 2 && (long)M * N >= 1536L * 768);
 }
 static int smer_wgrad256_depth() {
   static int v = -1;

@@ -1,4 +1,5 @@
-"""wgrad (+bias) shapes of the C2 step, isolated: per-launch time."""
+"""wgrad (+bias) shapes of the C2 / C4 step, isolated: per-launch time.
+    python tools/bench_wgrad.py [c2|c4]"""
 import os
 import sys
 
@@ -22,9 +23,15 @@ def timeit(fn, iters=20):
 
 
 bf = torch.bfloat16
-for (Mo, Nin, T) in ((512, 512, 8192), (2048, 512, 8192), (512, 2048, 8192), (1536, 512, 8192),
-                     (512, 512, 32768), (1024, 512, 32768), (2048, 512, 32768), (512, 2048, 32768),
-                     (1536, 512, 32768)):
+SHAPES = {
+    "c2": ((512, 512, 8192), (2048, 512, 8192), (512, 2048, 8192), (1536, 512, 8192),
+           (512, 512, 32768), (1024, 512, 32768), (2048, 512, 32768), (512, 2048, 32768),
+           (1536, 512, 32768)),
+    "c4": ((768, 768, 16384), (2304, 768, 16384), (3072, 768, 16384), (768, 3072, 16384),
+           (768, 768, 65536), (1536, 768, 65536), (2304, 768, 65536), (3072, 768, 65536),
+           (768, 3072, 65536)),
+}
+for (Mo, Nin, T) in SHAPES[sys.argv[1] if len(sys.argv) > 1 else "c2"]:
     dy = torch.randn(T, Mo, device="cuda").to(bf)
     x = torch.randn(T, Nin, device="cuda").to(bf)
     dw = torch.zeros(Mo, Nin, device="cuda")
