@@ -321,6 +321,33 @@ int smer_layernorm_fwd_fp8(int M, int N, const void* x, long ldx, const float* g
 int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, float* inv, unsigned* amax_next,
                     smer_stream_t stream);
 
+/* fp8 backward dgrads (C4, `train.py:783` differentiating the Linears of
+ * transformer.py:389,393,459,463,467): dX = dY . W runs as the NT product
+ * e4m3(dY) . e4m3(W^T)^T.
+ * smer_fp8_quantize_segments_t: seg is a DEVICE array of nseg x 4 int64
+ * (src bf16 [rows, cols] row-major, dst uint8 [cols, rows], rows, cols; rows
+ * and cols multiples of 64): dst = e4m3(src^T * 448 / amax|src|),
+ * inv_scale[s] = amax / 448 (current scaling, once per optimizer step).
+ * smer_gemm_fp8_ex: smer_gemm_fp8_q plus a ReLU gate (C = gv > 0 ? v *
+ * gate_scale : 0, exclusive with residual) for the FFN2 dgrad.
+ * smer_layernorm_bwd_fp8: smer_layernorm_bwd (bf16) plus the e4m3 copy
+ * q8 = e4m3(g * *qs) of the gradient that feeds the next dgrad (dx_drop when
+ * given, else dx), max|g| folded into *amax; partials_only != 0 writes the
+ * dgamma / dbeta partials only (smer_layernorm_param_reduce later). */
+int smer_fp8_quantize_segments_t(int nseg, const int64_t* seg, unsigned* amax_ws, float* inv_scale,
+                                 int blocks_per_seg, smer_stream_t stream);
+int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                     const float* a_inv, const float* b_inv, const float* bias, int relu,
+                     const void* residual, long ldr, const void* gate, long ldg, float gate_scale,
+                     float drop_p, uint32_t drop_seed, void* C, long ldc, void* q8, long ldq8,
+                     const float* qs, unsigned* amax, smer_stream_t stream);
+int smer_layernorm_bwd_fp8(int M, int N, const void* dy, long lddy, const void* x, long ldx,
+                           const float* mean, const float* rstd, const float* gamma, void* dx,
+                           long lddx, void* dx_drop, long ldxd, float drop_p, uint32_t seed,
+                           void* q8, long ldq, const float* qs, unsigned* amax, float* dgamma,
+                           float* dbeta, int accumulate, void* workspace, size_t ws_bytes,
+                           int partials_only, smer_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1915,8 +1915,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   GemmEpi ee = e;
   ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
   float amax_acc = 0.f;
-  const bf16* xsrc = (const bf16*)e.residual;
-  const long ldx = e.ldr;
+  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);  // streamed epilogue operand
+  const long ldx = e.residual ? e.ldr : e.ldg;
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;
@@ -2127,6 +2127,91 @@ extern "C" int smer_fp8_quantize_segments(int nseg, const int64_t* seg, unsigned
   return SMER_OK;
 }
 
+// Batched transposing e4m3 quantisation (the dgrad operands W^T of the fp8
+// backward): seg[4 s] = (src bf16 [rows, cols], dst uint8 [cols, rows], rows,
+// cols), rows and cols multiples of 64.  Per-tensor scale from the amax of
+// the whole tensor (transpose-invariant: the same scale as the forward copy).
+// A 256-thread block moves one 64 x 64 tile through LDS: rows read and
+// columns written 128 B at a time.
+__global__ __launch_bounds__(256) void amax_seg4_kernel(const int64_t* __restrict__ seg,
+                                                       unsigned int* __restrict__ amax) {
+  const int s = blockIdx.y;
+  const bf16* x = reinterpret_cast<const bf16*>(seg[4 * s]);
+  const long n8 = (seg[4 * s + 2] * seg[4 * s + 3]) >> 3;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + 8 * i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)v[k]));
+  }
+  m = wave_max(m);
+  __shared__ float wm_[4];
+  if ((threadIdx.x & 63) == 0) wm_[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(wm_[0], wm_[1]), fmaxf(wm_[2], wm_[3]));
+    atomicMax(amax + s, __float_as_uint(m));
+  }
+}
+
+__global__ __launch_bounds__(256) void quant_seg_t_kernel(const int64_t* __restrict__ seg,
+                                                         const unsigned int* __restrict__ amax,
+                                                         float* __restrict__ inv) {
+  __shared__ uint8_t t[64][72];
+  const int s = blockIdx.y;
+  const bf16* x = reinterpret_cast<const bf16*>(seg[4 * s]);
+  uint8_t* q = reinterpret_cast<uint8_t*>(seg[4 * s + 1]);
+  const int rows = (int)seg[4 * s + 2], cols = (int)seg[4 * s + 3];
+  const int tr = rows >> 6, tc = cols >> 6;
+  const float am = __uint_as_float(amax[s]);
+  const float sc = am > 0.f ? smer_div_rn(448.f, am) : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) inv[s] = smer_div_rn(1.f, sc);
+  const int tid = threadIdx.x;
+  for (int tile = blockIdx.x; tile < tr * tc; tile += gridDim.x) {
+    const int r0 = (tile / tc) * 64, c0 = (tile % tc) * 64;
+    // 64 rows x 8 chunks of 8 columns: 2 chunks per thread
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int item = tid + 256 * h, r = item >> 3, ch = item & 7;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long)(r0 + r) * cols + c0 + ch * 8);
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = (float)v[k];
+      const uint2 w = smer_q8x8(f, sc);
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(&w);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[ch * 8 + k][r] = b[k];
+    }
+    __syncthreads();
+    // dst rows c0 .. c0+63 (a source column each), 64 bytes: 8 x 8 B per row
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int item = tid + 256 * h, c = item >> 3, ch = item & 7;
+      uint2 w;
+      uint8_t* b = reinterpret_cast<uint8_t*>(&w);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = t[c][ch * 8 + k];
+      *reinterpret_cast<uint2*>(q + (long)(c0 + c) * rows + r0 + ch * 8) = w;
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int smer_fp8_quantize_segments_t(int nseg, const int64_t* seg, unsigned* amax_ws, float* inv_scale,
+                                            int blocks_per_seg, smer_stream_t stream) {
+  SMER_REQUIRE(nseg >= 0 && nseg <= 65535 && blocks_per_seg > 0, "smer_fp8_quantize_segments_t: sizes");
+  if (nseg == 0) return SMER_OK;
+  SMER_REQUIRE(seg && amax_ws && inv_scale, "smer_fp8_quantize_segments_t: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(amax_ws, 0, sizeof(unsigned) * nseg, s) != hipSuccess)
+    return smer_set_error(SMER_ERR_HIP, "smer_fp8_quantize_segments_t: memset");
+  const dim3 grid(blocks_per_seg, nseg);
+  hipLaunchKernelGGL(amax_seg4_kernel, grid, dim3(256), 0, s, seg, amax_ws);
+  hipLaunchKernelGGL(quant_seg_t_kernel, grid, dim3(256), 0, s, seg, (const unsigned*)amax_ws, inv_scale);
+  SMER_CHECK_LAUNCH("smer_fp8_quantize_segments_t");
+  return SMER_OK;
+}
+
 extern "C" size_t smer_fp8_quantize_workspace(void) { return 16; }
 
 extern "C" int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, void* q, long ldq,
@@ -2167,6 +2252,16 @@ extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, con
                                const void* residual, long ldr, float drop_p, uint32_t drop_seed,
                                void* C, long ldc, void* q8, long ldq8, const float* q8_scale,
                                unsigned* q8_amax, smer_stream_t stream) {
+  return smer_gemm_fp8_ex(M, N, K, A, lda, B, ldb, a_inv, b_inv, bias, relu, residual, ldr, nullptr, 0, 1.f,
+                          drop_p, drop_seed, C, ldc, q8, ldq8, q8_scale, q8_amax, stream);
+}
+
+extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                                const float* a_inv, const float* b_inv, const float* bias, int relu,
+                                const void* residual, long ldr, const void* gate, long ldg,
+                                float gate_scale, float drop_p, uint32_t drop_seed, void* C, long ldc,
+                                void* q8, long ldq8, const float* q8_scale, unsigned* q8_amax,
+                                smer_stream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % G2 || N % G2 || K % F8K)
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm_fp8: needs M, N % 256 == 0 and K % 128 == 0");
   SMER_REQUIRE(A && B && C && a_inv && b_inv, "smer_gemm_fp8: null pointer");
@@ -2178,8 +2273,10 @@ extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, con
   e.drop_thr = smer_drop_thr16(drop_p); e.seed = drop_seed;
   e.drop_scale = smer_drop_scale16(e.drop_thr);
   e.C = C; e.ldc = ldc;
+  e.gate = gate; e.ldg = ldg; e.gate_scale = gate_scale;
+  SMER_REQUIRE(!(gate && residual), "smer_gemm_fp8_ex: residual and gate are exclusive");
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
-  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc);
+  e.vec = a16(bias, 8) && a16(residual, ldr) && a16(gate, ldg) && a16(C, ldc);
   if (q8) {
     SMER_REQUIRE(e.vec && q8_scale && q8_amax && (((uintptr_t)q8) & 7) == 0 && ldq8 % 8 == 0,
                  "smer_gemm_fp8_q: fp8 output needs aligned vectors, scale and amax");

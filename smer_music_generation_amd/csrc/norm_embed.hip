@@ -202,7 +202,9 @@ static int ln_bwd_rows(int M, int N);  // below the kernel (needs its occupancy)
 // together (the rows are otherwise a chain of dependent HBM round trips at
 // 2 waves per SIMD).  Column partials for dgamma / dbeta accumulate in a
 // fixed row order (deterministic).
-template <typename T, bool DYF, int NC, int RB, bool PFB>
+// Q8 (fp8 backward): also the e4m3 copy of the stored gradient that feeds the
+// next dgrad (dxd when given, else dx) and its amax (delayed scaling, common.h)
+template <typename T, bool DYF, int NC, int RB, bool PFB, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* __restrict__ dyv,
                                                      long lddy, const T* __restrict__ x, long ldx,
                                                      const float* __restrict__ mean,
@@ -211,7 +213,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
                                                      T* __restrict__ dx, long lddx,
                                                      T* __restrict__ dxd, long ldxd,
                                                      uint32_t thr, uint32_t seed, float dscale,
-                                                     float* __restrict__ part, int rows_per_blk) {
+                                                     float* __restrict__ part, int rows_per_blk,
+                                                     uint8_t* __restrict__ q8 = nullptr, long ldq = 0,
+                                                     const float* __restrict__ qs_p = nullptr,
+                                                     unsigned* __restrict__ amax = nullptr) {
   constexpr int LN_MAXC = NC;
   __shared__ float red[4][2][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -225,6 +230,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
     for (int i = 0; i < 8; ++i) { pg[c][i] = 0.f; pb[c][i] = 0.f; }
   }
   const int r0 = blockIdx.x * rows_per_blk;
+  float q8s = 1.f, am = 0.f;
+  if constexpr (Q8) q8s = *qs_p;
   // bf16: the next batch's rows are fetched raw (16-B words, unclamped
   // statistics) before this batch's math, so a wave keeps two batches in
   // flight; every conversion / validity select happens at unpack time (a
@@ -348,10 +355,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
             if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)(ch * 8), o);
             Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
           }
+          if constexpr (Q8) {  // e4m3 copy of the stored (T-rounded) values
+            float r[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = (float)(T)o[i];
+            *reinterpret_cast<uint2*>(q8 + (long)row * ldq + ch * 8) = smer_q8x8(r, q8s);
+            am = fmaxf(am, smer_absmax8(r));
+          }
         }
       }
     }
   }
+  if constexpr (Q8) smer_amax_commit(amax, am);
   if (!part) return;
   // combine the 4 waves' column partials in fixed order, in <=512-col slabs
   for (int base = 0; base < N; base += 512) {
@@ -587,7 +602,7 @@ extern "C" int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, floa
 // raw before this batch's math.  Same per-element arithmetic, dropout
 // decisions (pair hashes of (row, col)) and partial layout as ln_bwd_kernel;
 // the row sums s1 / s2 add the lane's 12 columns in another order.
-template <int RB>
+template <int RB, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16* __restrict__ dy,
                                                         long lddy, const bf16* __restrict__ x, long ldx,
                                                         const float* __restrict__ mean,
@@ -596,7 +611,10 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
                                                         bf16* __restrict__ dx, long lddx,
                                                         bf16* __restrict__ dxd, long ldxd,
                                                         uint32_t thr, uint32_t seed, float dscale,
-                                                        float* __restrict__ part, int rows_per_blk) {
+                                                        float* __restrict__ part, int rows_per_blk,
+                                                        uint8_t* __restrict__ q8 = nullptr, long ldq = 0,
+                                                        const float* __restrict__ qs_p = nullptr,
+                                                        unsigned* __restrict__ amax = nullptr) {
   __shared__ float red[4][2][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c0 = 8 * lane, ct = 512 + 4 * lane;
@@ -612,6 +630,8 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
 #pragma unroll
   for (int i = 0; i < 12; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
   const int r0 = blockIdx.x * rows_per_blk;
+  float q8s = 1.f, am = 0.f;
+  if constexpr (Q8) q8s = *qs_p;
   uint4 px[RB], pd[RB];
   uint2 pxt[RB], pdt[RB];
   float pmu[RB], prs[RB];
@@ -716,8 +736,19 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
           *reinterpret_cast<bf16x4*>(dxd + (long)row * ldxd + ct) = wt;
         }
       }
+      if constexpr (Q8) {  // e4m3 copy of the last stored (bf16) values: w / wt
+        float r[8], rt[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = (float)w[i];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { rt[i] = tok ? (float)wt[i] : 0.f; rt[4 + i] = 0.f; }
+        *reinterpret_cast<uint2*>(q8 + (long)row * ldq + c0) = smer_q8x8(r, q8s);
+        am = fmaxf(am, fmaxf(smer_absmax8(r), smer_absmax8(rt)));
+        if (tok) *reinterpret_cast<uint32_t*>(q8 + (long)row * ldq + ct) = smer_q8x8(rt, q8s).x;
+      }
     }
   }
+  if constexpr (Q8) smer_amax_commit(amax, am);
   if (!part) return;
   // the 4 waves' column partials in fixed order: columns 0..511 in two
   // 256-column halves, then the tail
@@ -797,7 +828,8 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
                        const float* gamma, void* dx, long lddx, void* dx_drop, long ldxd,
                        float drop_p, uint32_t seed, float* dgamma, float* dbeta, int accumulate,
                        void* workspace, size_t ws_bytes, smer_stream_t stream, bool params,
-                       bool reduce) {
+                       bool reduce, uint8_t* q8 = nullptr, long ldq = 0, const float* qs = nullptr,
+                       unsigned* amax = nullptr) {
   SMER_REQUIRE(N % 8 == 0 && N <= 64 * 8 * LN_MAXC, "smer_layernorm_bwd: N % 8 == 0 and N <= 2048");
   SMER_REQUIRE(dx && dy && x && mean && rstd && gamma, "smer_layernorm_bwd: null pointer");
   SMER_REQUIRE(!params || (workspace && ws_bytes >= smer_layernorm_bwd_workspace(M, N)),
@@ -827,18 +859,47 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
     else if (N <= 1024) LNB1(T, F, 2, 2);          \
     else LNB1(T, F, 4, 1);                         \
   } while (0)
-  if (dtype == SMER_BF16 && !dy_f32 && ln_bwd_t4_shape(N) && ln_bwd_t4_enabled() &&
-      ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
-      ((uintptr_t)dx_drop & 15) == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && ldxd % 8 == 0) {
-    hipLaunchKernelGGL((ln_bwd_t4_kernel<4>), dim3(nblk), dim3(256), 0, s, M, N, (const bf16*)dy, lddy,
-                       (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop, ldxd,
-                       thr, seed, ds, part, rpb);
+  if (q8) {
+    SMER_REQUIRE(dtype == SMER_BF16 && !dy_f32 && qs && amax && ((uintptr_t)q8 & 7) == 0 && ldq % 8 == 0,
+                 "smer_layernorm_bwd_fp8: bf16 dy, aligned q8, scale and amax");
+    SMER_REQUIRE(((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+                     ((uintptr_t)dx_drop & 15) == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 &&
+                     ldxd % 8 == 0,
+                 "smer_layernorm_bwd_fp8: 16-B aligned rows");
+  }
+  const bool t4 = dtype == SMER_BF16 && !dy_f32 && ln_bwd_t4_shape(N) && ln_bwd_t4_enabled() &&
+                  ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
+                  ((uintptr_t)dx_drop & 15) == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 &&
+                  ldxd % 8 == 0;
+#define LNBT4(Q)                                                                                           \
+  hipLaunchKernelGGL((ln_bwd_t4_kernel<4, Q>), dim3(nblk), dim3(256), 0, s, M, N, (const bf16*)dy, lddy,    \
+                     (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop, ldxd, thr,    \
+                     seed, ds, part, rpb, q8, ldq, qs, amax)
+#define LNBQ(NC, RB, PF)                                                                                   \
+  hipLaunchKernelGGL((ln_bwd_kernel<bf16, false, NC, RB, PF, true>), dim3(nblk), dim3(256), 0, s, M, N,    \
+                     dy, lddy, (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop,    \
+                     ldxd, thr, seed, ds, part, rpb, q8, ldq, qs, amax)
+#define LNBQ1(NC, RB)                                  \
+  do {                                                 \
+    if (rpb / 4 > (RB)) LNBQ(NC, RB, true);            \
+    else LNBQ(NC, RB, false);                          \
+  } while (0)
+  if (q8) {
+    if (t4) LNBT4(true);
+    else if (N <= 512) LNBQ1(1, 4);
+    else if (N <= 1024) LNBQ1(2, 2);
+    else LNBQ1(4, 1);
+  } else if (t4) {
+    LNBT4(false);
   } else if (dtype == SMER_BF16) { if (dy_f32) LNB(bf16, true); else LNB(bf16, false); }
   else if (dtype == SMER_F32) { LNB(float, false); }
   else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_layernorm_bwd: dtype");
 #undef LNB
 #undef LNB1
 #undef LNB2
+#undef LNBT4
+#undef LNBQ
+#undef LNBQ1
   if (reduce) {
     if (dgamma && dbeta)  // both vectors in one reduction over the [nblk][2N] partials
       smer_col_reduce_launch(nblk, 2 * N, part, (long)2 * N, 0L, dgamma, accumulate, 1.f,
@@ -875,6 +936,20 @@ extern "C" int smer_layernorm_bwd_partials(int dtype, int M, int N, const void* 
   return ln_bwd_impl(dtype, M, N, dy, lddy, dy_f32, x, ldx, mean, rstd, gamma, dx, lddx, dx_drop,
                      ldxd, drop_p, seed, nullptr, nullptr, 0, workspace, ws_bytes, stream, true,
                      false);
+}
+
+extern "C" int smer_layernorm_bwd_fp8(int M, int N, const void* dy, long lddy, const void* x, long ldx,
+                                      const float* mean, const float* rstd, const float* gamma, void* dx,
+                                      long lddx, void* dx_drop, long ldxd, float drop_p, uint32_t seed,
+                                      void* q8, long ldq, const float* qs, unsigned* amax, float* dgamma,
+                                      float* dbeta, int accumulate, void* workspace, size_t ws_bytes,
+                                      int partials_only, smer_stream_t stream) {
+  SMER_REQUIRE(q8, "smer_layernorm_bwd_fp8: q8 required");
+  SMER_REQUIRE(!partials_only || workspace, "smer_layernorm_bwd_fp8: partials need a workspace");
+  const bool params = partials_only || dgamma || dbeta;
+  return ln_bwd_impl(SMER_BF16, M, N, dy, lddy, 0, x, ldx, mean, rstd, gamma, dx, lddx, dx_drop, ldxd,
+                     drop_p, seed, dgamma, dbeta, accumulate, workspace, ws_bytes, stream, params,
+                     !partials_only, (uint8_t*)q8, ldq, qs, amax);
 }
 
 extern "C" int smer_layernorm_param_reduce(int M, int N, void* workspace, size_t ws_bytes,

@@ -316,6 +316,7 @@ class Engine:
                 self._fp8 = Fp8Forward(self, dev)
             f8 = self._fp8
             f8.begin(W, training=training)
+        ctx.f8 = f8 if (training and save) else None
         x = torch.empty(B * S, d, dtype=dt, device=dev)
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
         xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)
@@ -434,6 +435,43 @@ class Engine:
         G = self.grad_views()
         Mt, Ms = B * T, B * S
 
+        from .fp8 import FP8_DGRAD, eligible
+        f8 = ctx.f8 if FP8_DGRAD else None
+
+        def ln_bwd(g_in, y_, mu, rs, wb, dx_, dxd_, seed_, gw, site):
+            """LayerNorm backward; in fp8 mode also the e4m3 copy of the gradient
+            feeding the next dgrad: returns (q8, site) once the site's scale has
+            a step of history, else None."""
+            kw = dict(dx_drop=dxd_ if p_tr > 0 else None, drop_p=p_tr, seed=seed_, dgamma=gw[0],
+                      dbeta=gw[1], param_stream=ps)
+            if f8 is None:
+                ops.layernorm_bwd(g_in, y_, mu, rs, wb[0], dx_, **kw)
+                return None
+            si = f8.site(site)
+            q = torch.empty(y_.shape, dtype=torch.uint8, device=dev)
+            ops.layernorm_bwd(g_in, y_, mu, rs, wb[0], dx_, q8=q, qs=f8.qs_of(si), amax=f8.amax_of(si), **kw)
+            f8.record_bwd(site)
+            return (q, si) if site in f8.bwd_ready else None
+
+        def dgrad(gq, g, wname, w, q_site=None, **epi):
+            """g @ w; on the fp8 MFMA (e4m3(g) . e4m3(w^T)^T) when g has a usable
+            e4m3 copy gq.  q_site: also the e4m3 copy of the output."""
+            M = g.shape[0]
+            if gq is not None:
+                wt = f8.weight_t(wname)
+                if wt is not None and eligible(M, w.shape[1], w.shape[0]):
+                    out = torch.empty(M, w.shape[1], dtype=dt, device=dev)
+                    if q_site is None:
+                        ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, **epi)
+                        return out, None
+                    si = f8.site(q_site)
+                    q = torch.empty(M, w.shape[1], dtype=torch.uint8, device=dev)
+                    ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, q8=q, qs=f8.qs_of(si),
+                                    amax=f8.amax_of(si), **epi)
+                    f8.record_bwd(q_site)
+                    return out, ((q, si) if q_site in f8.bwd_ready else None)
+            return ops.linear_dgrad(g, w, **epi), None
+
         # vocab head
         side = self._wgrad_stream(dev, dt)
         ps = side[0] if side is not None else None  # LayerNorm dgamma / dbeta reductions too
@@ -458,21 +496,18 @@ class Engine:
             # FFN block: x3 = LN3(x2 + drop(W2 drop(relu(W1 x2))))
             dy3 = torch.empty_like(y3)
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
-            ops.layernorm_bwd(dy, y3, m3, r3, L.n3[0], dy3, dx_drop=dy3d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 5)), dgamma=GL.n3[0], dbeta=GL.n3[1],
-                              param_stream=ps)
+            dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
             wg(dy3d, h, GL.l2_w, db=GL.l2_b)
-            dh = ops.linear_dgrad(dy3d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
+            dh, dhq = dgrad(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, q_site="b.dec%d.dh" % i, gate=h,
+                            gate_scale=ops.drop_scale(p_tr))
             wg(dh, x2, GL.l1_w, db=GL.l1_b)
-            dx2 = ops.linear_dgrad(dh, L.l1_w, residual=dy3)
+            dx2, _ = dgrad(dhq, dh, "dec%d.l1" % i, L.l1_w, residual=dy3)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
-            ops.layernorm_bwd(dx2, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1],
-                              param_stream=ps)
+            dy2q = ln_bwd(dx2, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("dec", i, 3)), GL.n2, "b.dec%d.ln2" % i)
             wg(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
-            doc = ops.linear_dgrad(dy2d, L.ca_ow)
+            doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
@@ -484,11 +519,9 @@ class Engine:
             # self-attention block
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
-            ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("dec", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1],
-                              param_stream=ps)
+            dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("dec", i, 1)), GL.n1, "b.dec%d.ln1" % i)
             wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
-            do = ops.linear_dgrad(dy1d, L.sa_ow)
+            do, _ = dgrad(dy1q, dy1d, "dec%d.sao" % i, L.sa_ow)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
@@ -514,20 +547,17 @@ class Engine:
             (x_in, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2) = ctx.enc[i]
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
-            ops.layernorm_bwd(dx, y2, m2, r2, L.n2[0], dy2, dx_drop=dy2d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("enc", i, 3)), dgamma=GL.n2[0], dbeta=GL.n2[1],
-                              param_stream=ps)
+            dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
             wg(dy2d, h, GL.l2_w, db=GL.l2_b)
-            dh = ops.linear_dgrad(dy2d, L.l2_w, gate=h, gate_scale=ops.drop_scale(p_tr))
+            dh, dhq = dgrad(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, q_site="b.enc%d.dh" % i, gate=h,
+                            gate_scale=ops.drop_scale(p_tr))
             wg(dh, x1, GL.l1_w, db=GL.l1_b)
-            dx1 = ops.linear_dgrad(dh, L.l1_w, residual=dy2)
+            dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
-            ops.layernorm_bwd(dx1, y1, m1, r1, L.n1[0], dy1, dx_drop=dy1d if p_tr > 0 else None,
-                              drop_p=p_tr, seed=sd(_site("enc", i, 1)), dgamma=GL.n1[0], dbeta=GL.n1[1],
-                              param_stream=ps)
+            dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("enc", i, 1)), GL.n1, "b.enc%d.ln1" % i)
             wg(dy1d, o, GL.out_w, db=GL.out_b)
-            do = ops.linear_dgrad(dy1d, L.out_w)
+            do, _ = dgrad(dy1q, dy1d, "enc%d.out" % i, L.out_w)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,

@@ -7,8 +7,20 @@ in-projections of layers >= 1, FFN1, the decoder's cross-attention Q and the
 stacked cross-attention K/V of the memory (`transformer.py:389,393,459,463,
 467`); FFN2 too when FFN1 writes an e4m3 copy of its output
 (engine.FP8_FFN2, off by default: measured slower at C4).  Out-projections
-(input: attention output), the vocab head and every backward GEMM stay bf16;
-master weights fp32, working weights bf16.
+(input: attention output) and the vocab head stay bf16; master weights fp32,
+working weights bf16.
+
+Backward (FP8_DGRAD): the dgrad products whose input gradient comes from a
+LayerNorm backward or from the FFN2 dgrad run as e4m3(dY) . e4m3(W^T)^T on
+the same kernel: FFN2 dgrad (ReLU gate in the epilogue, writing the e4m3
+copy of dh), FFN1 dgrad (residual) and the attention out-projection dgrads.
+The LayerNorm backward writes the gradient's e4m3 copy beside its bf16
+output; scales are delayed like the forward's (the amax recorded in step
+t - 1), so a backward site switches to fp8 once it has one step of
+history (the first step's backward is bf16).  W^T copies are quantised with
+the forward copies, once per optimizer step.  QKV / cross-Q dgrads (input:
+the attention backward), the memory dgrad and every weight gradient stay
+bf16.
 
 Scaling (no standalone quantise pass over activations):
   * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy
@@ -24,11 +36,15 @@ Scaling (no standalone quantise pass over activations):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
 
 N_SITES = 512
+# fp8 backward dgrads (SMER_FP8_DGRAD=0: bf16 backward, A/B and tests)
+FP8_DGRAD = os.environ.get("SMER_FP8_DGRAD", "1") != "0"
 
 
 class Fp8Forward:
@@ -48,6 +64,10 @@ class Fp8Forward:
         self._w = {}
         self._wbuf = {}       # name -> (e4m3 buffer, inv view), persistent
         self._seg = None      # (key, device seg table, amax workspace, inv)
+        self._wt = {}         # name -> (e4m3 W^T buffer, inv view), persistent
+        self._segt = None
+        self._bwd_recorded = set()  # backward sites whose amax this step records
+        self.bwd_ready = set()      # ... recorded in an earlier step: scales valid
 
     def begin(self, W=None, training=True):
         """Start a forward: this forward's scales from the previous one's
@@ -63,6 +83,8 @@ class Fp8Forward:
         calibrate = training or not self.trained
         self.trained = self.trained or training
         if calibrate:
+            self.bwd_ready |= self._bwd_recorded
+            self._bwd_recorded = set()
             prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
             ops.fp8_scales(prev, self.qs, self.inv, nxt)
             self.cur = nxt
@@ -85,6 +107,49 @@ class Fp8Forward:
             out.append(("ckv", W.ckv_all))
         return out
 
+    @staticmethod
+    def dgrad_weights(W):
+        """(name, bf16 weight [out, in]) of every dgrad that runs on the fp8
+        MFMA (as e4m3(dY) . e4m3(W^T)^T)."""
+        out = []
+        for i, L in enumerate(W.enc):
+            out += [("enc%d.out" % i, L.out_w), ("enc%d.l1" % i, L.l1_w), ("enc%d.l2" % i, L.l2_w)]
+        for i, L in enumerate(W.dec):
+            out += [("dec%d.sao" % i, L.sa_ow), ("dec%d.cao" % i, L.ca_ow), ("dec%d.l1" % i, L.l1_w),
+                    ("dec%d.l2" % i, L.l2_w)]
+        return out
+
+    def _quantize_weights_t(self, W):
+        ws = [(n, w) for n, w in self.dgrad_weights(W)
+              if w.is_contiguous() and w.dim() == 2 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0]
+        key = tuple((n, w.data_ptr(), tuple(w.shape)) for n, w in ws)
+        if self._segt is None or self._segt[0] != key:
+            rows = []
+            for n, w in ws:
+                buf = self._wt.get(n)
+                if buf is None or buf[0].shape != (w.shape[1], w.shape[0]):
+                    buf = (torch.empty(w.shape[1], w.shape[0], dtype=torch.uint8, device=self.dev), None)
+                rows.append((w.data_ptr(), buf[0].data_ptr(), w.shape[0], w.shape[1]))
+                self._wt[n] = buf
+            host = torch.tensor(rows, dtype=torch.int64).pin_memory() if rows else None
+            seg = (torch.empty_like(host, device=self.dev).copy_(host, non_blocking=True)
+                   if rows else None)
+            inv = torch.ones(max(1, len(ws)), device=self.dev)
+            amax_ws = torch.zeros(max(1, len(ws)), dtype=torch.int32, device=self.dev)
+            self._segt = (key, seg, amax_ws, inv, host)
+            self._wt = {n: (self._wt[n][0], inv[k:k + 1]) for k, (n, _) in enumerate(ws)}
+        _, seg, amax_ws, inv, _ = self._segt
+        if seg is not None:
+            ops.fp8_quantize_segments_t(seg, amax_ws, inv)
+
+    def weight_t(self, name):
+        """(e4m3 W^T, inv scale) of a dgrad weight, or None."""
+        return self._wt.get(name)
+
+    def record_bwd(self, name):
+        """A backward producer wrote site `name`'s amax this step."""
+        self._bwd_recorded.add(name)
+
     def _quantize_weights(self, W):
         ws = [(n, w) for n, w in self.gemm_weights(W) if w.is_contiguous() and w.numel() % 8 == 0]
         key = tuple((n, w.data_ptr(), w.numel()) for n, w in ws)
@@ -104,6 +169,8 @@ class Fp8Forward:
         _, seg, amax_ws, inv, _ = self._seg
         ops.fp8_quantize_segments(seg, amax_ws, inv)
         self._w = {n: (self._wbuf[n], inv[k:k + 1]) for k, (n, _) in enumerate(ws)}
+        if FP8_DGRAD:
+            self._quantize_weights_t(W)
         self._wkey = self.eng._wgen
 
     def finite(self):

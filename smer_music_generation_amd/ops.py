@@ -331,6 +331,43 @@ def fp8_quantize_segments(seg, amax_ws, inv, blocks_per_seg=64):
          _stream())
 
 
+def fp8_quantize_segments_t(seg, amax_ws, inv, blocks_per_seg=64):
+    """Batched transposing e4m3 quantisation: seg int64 [nseg, 4] on the
+    device = (src bf16 ptr [rows, cols], dst uint8 ptr [cols, rows], rows,
+    cols), rows / cols multiples of 64; inv fp32 [nseg] <- amax / 448."""
+    n = seg.shape[0]
+    if amax_ws.numel() < n or inv.numel() < n:
+        raise ValueError("fp8_quantize_segments_t: workspace / inv smaller than nseg")
+    call("smer_fp8_quantize_segments_t", n, _p(seg), _p(amax_ws), _p(inv), int(blocks_per_seg),
+         _stream())
+
+
+def gemm_fp8_ex(a8, a_inv, b8, b_inv, out, *, bias=None, residual=None, gate=None, gate_scale=1.0,
+                q8=None, qs=None, amax=None):
+    """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ bias) (+ residual | ReLU gate:
+    out = gate > 0 ? v * gate_scale : 0), optionally with the e4m3 copy of out
+    (q8 = e4m3(out * qs), max|out| folded into amax).  The fp8 backward's
+    dgrad products.  Returns False (nothing launched) outside the tiling."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    if M % 256 or N % 256 or K % 128:
+        return False
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    call("smer_gemm_fp8_ex", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
+         _p(bias), 0, _p(residual), _ld(residual) if residual is not None else 0, _p(gate),
+         _ld(gate) if gate is not None else 0, float(gate_scale), 0.0, 0, _p(out), _ld(out), _p(q8),
+         _ld(q8) if q8 is not None else 0, _p(qs), _p(amax), _stream())
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * K, "fp8 dgrad M%d N%d K%d%s" % (
+            M, N, K, " g" if gate is not None else " R" if residual is not None else "")))
+    return True
+
+
 def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
              seed=0):
     """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ epilogue).  Returns False
@@ -425,13 +462,32 @@ def layernorm(x, gamma, beta, y, mean, rstd, eps=1e-5):
 
 
 def layernorm_bwd(dy, x, mean, rstd, gamma, dx, *, dx_drop=None, drop_p=0.0, seed=0,
-                  dgamma=None, dbeta=None, accumulate=True, param_stream=None):
+                  dgamma=None, dbeta=None, accumulate=True, param_stream=None, q8=None, qs=None,
+                  amax=None):
     """param_stream: run the dgamma / dbeta column reduction on that stream
-    (after this stream's LayerNorm kernel), off the dgrad chain."""
+    (after this stream's LayerNorm kernel), off the dgrad chain.  q8 (bf16
+    only): also the e4m3 copy e4m3(g * qs) of the gradient g that feeds the
+    next dgrad (dx_drop when given, else dx), max|g| folded into amax."""
     lib = load()
     M, N = x.shape
     nbytes = lib.smer_layernorm_bwd_workspace(M, N) if (dgamma is not None or dbeta is not None) else 0
     ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=x.device)
+    if q8 is not None:
+        if x.dtype != torch.bfloat16 or dy.dtype != torch.bfloat16:
+            raise RuntimeError("layernorm_bwd: the e4m3 copy needs bf16 dy and x")
+        partial = param_stream is not None and nbytes > 0
+        call("smer_layernorm_bwd_fp8", M, N, _p(dy), _ld(dy), _p(x), _ld(x), _p(mean), _p(rstd),
+             _p(gamma), _p(dx), _ld(dx), _p(dx_drop), _ld(dx_drop) if dx_drop is not None else 0,
+             float(drop_p), int(seed) & 0xFFFFFFFF, _p(q8), _ld(q8), _p(qs), _p(amax),
+             _p(None if partial else dgamma), _p(None if partial else dbeta), int(accumulate),
+             _p(ws), nbytes, int(partial), _stream())
+        if partial:
+            param_stream.wait_stream(torch.cuda.current_stream(x.device))
+            with torch.cuda.stream(param_stream):
+                call("smer_layernorm_param_reduce", M, N, _p(ws), nbytes, _p(dgamma), _p(dbeta),
+                     int(accumulate), _stream())
+            ws.record_stream(param_stream)
+        return
     if param_stream is not None and nbytes:
         call("smer_layernorm_bwd_partials", dtype_code(x.dtype), M, N, _p(dy), _ld(dy),
              int(dy.dtype == torch.float32 and x.dtype != torch.float32), _p(x), _ld(x), _p(mean),
