@@ -366,7 +366,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
       }
     }
   }
-  if constexpr (Q8) smer_amax_commit(amax, am);
+  if constexpr (Q8) {  // one atomic per workgroup (per wave: 16k waves contend on one address)
+    __shared__ float wam[4];
+    am = wave_max(am);
+    if (lane == 0) wam[wave] = am;
+    __syncthreads();
+    if (threadIdx.x < 64) smer_amax_commit(amax, lane < 4 ? wam[lane] : 0.f);
+  }
   if (!part) return;
   // combine the 4 waves' column partials in fixed order, in <=512-col slabs
   for (int base = 0; base < N; base += 512) {
@@ -748,7 +754,13 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
       }
     }
   }
-  if constexpr (Q8) smer_amax_commit(amax, am);
+  if constexpr (Q8) {  // one atomic per workgroup (per wave: 16k waves contend on one address)
+    __shared__ float wam[4];
+    am = wave_max(am);
+    if (lane == 0) wam[wave] = am;
+    __syncthreads();
+    if (threadIdx.x < 64) smer_amax_commit(amax, lane < 4 ? wam[lane] : 0.f);
+  }
   if (!part) return;
   // the 4 waves' column partials in fixed order: columns 0..511 in two
   // 256-column halves, then the tail
@@ -785,6 +797,13 @@ static bool ln_bwd_t4_enabled() {
   return !(e && e[0] == '0');
 }
 static inline bool ln_bwd_t4_shape(int N) { return N > 512 && N <= 768 && N % 4 == 0; }
+// rows per batch of ln_bwd_t4_kernel: 4, or 2 with the e4m3 copy (65536 x
+// 768: 94.5 vs 95.7 us without it, 105.0 vs 109.7 with it, tools/ln_bench.py);
+// SMER_LN_BWD_T4_RB = 2 / 4 forces it (A/B runs)
+static int ln_bwd_t4_rb(bool q8) {
+  const char* e = getenv("SMER_LN_BWD_T4_RB");  // per call: A/B scripts flip it in-process
+  return e ? (e[0] == '2' ? 2 : 4) : (q8 ? 2 : 4);
+}
 
 // Rows per workgroup.  N > 512 at large M (C4: 65536 x 768): 64-row blocks
 // made 1024 workgroups for ~768 resident slots (3 per CU at that register
@@ -871,10 +890,15 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
                   ((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dx & 15) == 0 &&
                   ((uintptr_t)dx_drop & 15) == 0 && lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 &&
                   ldxd % 8 == 0;
-#define LNBT4(Q)                                                                                           \
-  hipLaunchKernelGGL((ln_bwd_t4_kernel<4, Q>), dim3(nblk), dim3(256), 0, s, M, N, (const bf16*)dy, lddy,    \
+#define LNBT4R(R, Q)                                                                                       \
+  hipLaunchKernelGGL((ln_bwd_t4_kernel<R, Q>), dim3(nblk), dim3(256), 0, s, M, N, (const bf16*)dy, lddy,    \
                      (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop, ldxd, thr,    \
                      seed, ds, part, rpb, q8, ldq, qs, amax)
+#define LNBT4(Q)                                         \
+  do {                                                   \
+    if (ln_bwd_t4_rb(Q) == 2) LNBT4R(2, Q);              \
+    else LNBT4R(4, Q);                                   \
+  } while (0)
 #define LNBQ(NC, RB, PF)                                                                                   \
   hipLaunchKernelGGL((ln_bwd_kernel<bf16, false, NC, RB, PF, true>), dim3(nblk), dim3(256), 0, s, M, N,    \
                      dy, lddy, (const bf16*)x, ldx, mean, rstd, gamma, (bf16*)dx, lddx, (bf16*)dx_drop,    \
@@ -898,6 +922,7 @@ static int ln_bwd_impl(int dtype, int M, int N, const void* dy, long lddy, int d
 #undef LNB1
 #undef LNB2
 #undef LNBT4
+#undef LNBT4R
 #undef LNBQ
 #undef LNBQ1
   if (reduce) {

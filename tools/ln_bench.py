@@ -37,6 +37,12 @@ for M, N in ((32768, 512), (8192, 512), (65536, 768), (16384, 768)):
     tf = timeit(lambda: ops.layernorm(x, g, b, y, mean, rstd))
     tb = timeit(lambda: ops.layernorm_bwd(dy, x, mean, rstd, g, dx, dx_drop=dxd, drop_p=0.1, seed=3,
                                           dgamma=dg, dbeta=db))
+    q8 = torch.empty(M, N, dtype=torch.uint8, device=dev)
+    qs = torch.ones(1, device=dev)
+    am = torch.zeros(1, dtype=torch.int32, device=dev)
+    tq = timeit(lambda: ops.layernorm_bwd(dy, x, mean, rstd, g, dx, dx_drop=dxd, drop_p=0.1, seed=3,
+                                          dgamma=dg, dbeta=db, q8=q8, qs=qs, amax=am))
+    print("M=%d N=%d bwd with the e4m3 gradient copy %.1f us" % (M, N, tq), flush=True)
     fb = 2 * M * N * 2 / tf / 1e3
     bb = 4 * M * N * 2 / tb / 1e3
     print("M=%d N=%d fwd %.1f us (%.0f GB/s)  bwd %.1f us (%.0f GB/s)" % (M, N, tf, fb, tb, bb), flush=True)

@@ -33,6 +33,9 @@ for p in fp8 bf16; do
   SMER_WGRAD_OVERLAP=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4_$p -o run -- \
     python3 $R/tools/c4_step.py $p 4 > $OUT/c4_$p.log 2>&1
 done
+# C4 fp8 with the weight gradients serialised: each kernel's own duration
+SMER_WGRAD_OVERLAP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4ser -o run -- \
+  python3 $R/tools/c4_step.py fp8 4 > $OUT/c4ser.log 2>&1
 bash $R/tools/profile_pmc.sh $TAG > $OUT/pmc_sq.log 2>&1
 bash $R/tools/pmc_fp8_gemm.sh > $OUT/pmc_fp8.log 2>&1
 echo done

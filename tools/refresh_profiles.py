@@ -85,6 +85,23 @@ for p in ("fp8", "bf16"):
                     "layers d768 h12 S2048 T512 B32; weight gradients on the side stream; 5 steps "
                     "traced; per-step = total/5)\n" % p + t)
 
+c = os.path.join(src, "c4ser", "run_kernel_stats.csv")
+if os.path.exists(c):
+    t = run(os.path.join(ROOT, "tools", "prof_summary.py"), c, "5", "30")
+    with open(os.path.join(dst, "%s_c4_fp8_serial_kernel_stats.txt" % tag), "w") as f:
+        f.write("# SMER_WGRAD_OVERLAP=0 rocprofv3 --kernel-trace --stats -- python3 tools/c4_step.py fp8 4 "
+                "(C4 fp8, weight gradients serialised on the main stream: each kernel's own duration; "
+                "5 steps traced; per-step = total/5)\n" + t)
+
+# per-stream busy time of the overlapped traces (tools/stream_split.py)
+for name, sub in (("train_stream_split", "trace_ovl"), ("c4_fp8_stream_split", "c4_fp8")):
+    tr = os.path.join(src, sub, "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        t = run(os.path.join(ROOT, "tools", "stream_split.py"), tr, "3")
+        with open(os.path.join(dst, "%s_%s.txt" % (tag, name)), "w") as f:
+            f.write("# tools/stream_split.py over the last 3 traced steps of %s (stream 0 = the dgrad "
+                    "chain, stream 1 = weight gradients)\n" % sub + t)
+
 # SQ counters (train step, weight gradients serialised) and the fp8 GEMM pair
 for name, sub in (("train_pmc_sq", os.path.join("..", "pmc_" + tag, "sq.txt")),
                   ("fp8_gemm_pmc_sq", os.path.join("..", "pmc_fp8", "sq.txt"))):
