@@ -165,6 +165,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
   // per-key additive score bias of the staged tile: 0, or -inf for padded /
   // out-of-range keys; it seeds the S accumulators, so masking costs no VALU
   __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
+  __shared__ int kpad[2];  // the staged tile has a padded / out-of-range key
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
@@ -176,6 +177,8 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
   // SWAR threshold word for smer_attn_ge (drop_thr = thr7)
   const uint32_t lo4 = drop_thr * 0x01010101u;
 
+  // Q pre-scaled by c = scale * log2(e) (once, in registers): the scores
+  // leave the MFMA in log2 units, so p = 2^(s - m) needs no multiply
   bf16x8 qf[QG][C::NS];
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
@@ -196,13 +199,23 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     int qmax = min(Lq, BX * QB + QB);
     n_tiles = min(n_tiles, (qmax + KVB - 1) / KVB);
   }
-  float m_run[QG], l_run[QG];
+  // Online softmax against a per-query reference m_ref (log2 units, always
+  // finite): acc and l hold sums of 2^(s - m_ref).  The QK^T chain starts
+  // from -m_ref, so a tile whose scores all stay within 2^THR of the
+  // reference is exponentiated as it leaves the MFMA; only a tile that
+  // raises some query's max past that (or brings a query its first
+  // unmasked key) moves the reference and rescales (deferred max).
+  constexpr float THR = 8.f;
+  float m_run[QG], m_ref[QG], l_run[QG];
+  f32x4 negm[QG];
   uint32_t rowkey[QG];
   f32x4 acc[QG][C::NDT];
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     rowkey[gq] = DROP ? smer_rowkey(seed, (uint32_t)(bh * Lq + q0w + gq * 16 + c16)) : 0u;
     m_run[gq] = -INFINITY;
+    m_ref[gq] = 0.f;
+    negm[gq] = f32x4{0.f, 0.f, 0.f, 0.f};
     l_run[gq] = 0.f;
 #pragma unroll
     for (int i = 0; i < C::NDT; ++i) acc[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -217,10 +230,21 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
-    if (tid < KVB) kbias[0][tid] = key_bias(tid);
+    if (tid < KVB) {  // wave 0
+      const float kbz = key_bias(tid);
+      kbias[0][tid] = kbz;
+      const uint64_t any = __ballot(kbz != 0.f);
+      if (tid == 0) kpad[0] = any != 0ull;
+    }
   }
   __syncthreads();
   smer_vm_drain();  // prologue loads retired before the loop (common.h)
+#pragma unroll
+  for (int gq = 0; gq < QG; ++gq)
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[gq][s][e] = (bf16)((float)qf[gq][s][e] * c);
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
@@ -246,9 +270,8 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     f32x4 st[QG][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
 #pragma unroll
-      for (int gq = 0; gq < QG; ++gq) st[gq][mt] = kbv;
+      for (int gq = 0; gq < QG; ++gq) st[gq][mt] = negm[gq];
 #pragma unroll
       for (int s = 0; s < C::NS; ++s) {
         const bf16x8 kf = row_frag<D>(Ks, mt * 16, s, lane);
@@ -256,11 +279,19 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
         for (int gq = 0; gq < QG; ++gq) st[gq][mt] = mfma16(kf, qf[gq][s], st[gq][mt]);
       }
     }
+    if (__builtin_amdgcn_readfirstlane(kpad[cur])) {
+      // -inf on padded / out-of-range keys (tiles without any skip this)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) st[gq][mt] += kbv;
+      }
+    }
     bf16x8 pf[QG][2];
 #pragma unroll
     for (int gq = 0; gq < QG; ++gq) {
       const int qi = q0w + gq * 16 + c16;
-      // max in raw score units (c > 0), exponent as one fma: p = 2^(s*c - m*c)
       if (causal && t * KVB + KVB - 1 > q0w + gq * 16) {
         // key - query = kq0 + 16mt + r: one difference, immediate offsets
         const int kq0 = t * KVB + 4 * g - qi;
@@ -270,28 +301,37 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
           for (int r = 0; r < 4; ++r)
             if (kq0 > -(mt * 16 + r)) st[gq][mt][r] = -INFINITY;
       }
+      // this lane's tile max, relative to m_ref
       float tmax = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, st[gq][mt][r]);
-      tmax = max_4groups(tmax);
-      const float m_new = fmaxf(m_run[gq], tmax);
-      const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      // lazy rescale: skip the accumulator multiply while no lane's max moved
-      if (__ballot(m_new > m_run[gq]) != 0ull) {
-        const float alpha = fast_exp2((m_run[gq] - m_use) * c);
+      const bool moved = tmax > THR || (m_run[gq] == -INFINITY && tmax != -INFINITY);
+      if (__ballot(moved) != 0ull) {
+        // the query's tile max over its 4 lane groups; m_ref follows the
+        // running max once the query has seen a key (a no-op for lanes
+        // whose max did not move: d = 0)
+        const float gmax = max_4groups(tmax) + m_ref[gq];
+        const float m_new = fmaxf(m_run[gq], gmax);
+        const float ref = m_new == -INFINITY ? m_ref[gq] : m_new;
+        const float d = ref - m_ref[gq];
+        const float alpha = fast_exp2(-d);
         l_run[gq] *= alpha;
 #pragma unroll
         for (int i = 0; i < C::NDT; ++i) acc[gq][i] *= alpha;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) st[gq][mt] -= d;
+        m_run[gq] = m_new;
+        m_ref[gq] = ref;
+        negm[gq] = f32x4{-ref, -ref, -ref, -ref};
       }
-      const float mc = m_use * c;
       float p[4][4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[mt][r] = fast_exp2(fmaf(st[gq][mt][r], c, -mc));
+          p[mt][r] = fast_exp2(st[gq][mt][r]);
           l_run[gq] += p[mt][r];
         }
       // P as bf16 pairs: word [mt][0] = keys (r0, r1), [mt][1] = (r2, r3).
@@ -330,7 +370,6 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
           reinterpret_cast<uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane] =
               (uint16_t)attn_fold_keep(kacc);
       }
-      m_run[gq] = m_new;
       pf[gq][0] = words_bf16x8(pw[0][0], pw[0][1], pw[1][0], pw[1][1]);
       pf[gq][1] = words_bf16x8(pw[2][0], pw[2][1], pw[3][0], pw[3][1]);
     }
@@ -347,7 +386,12 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
       asm volatile("" : "+v"(npad));  // keeps the compare (and its wait) here
-      if (tid < KVB) kbias[cur ^ 1][tid] = ((t + 1) * KVB + tid >= Lk || npad) ? -INFINITY : 0.f;
+      if (tid < KVB) {  // wave 0
+        const bool pk = (t + 1) * KVB + tid >= Lk || npad;
+        kbias[cur ^ 1][tid] = pk ? -INFINITY : 0.f;
+        const uint64_t any = __ballot(pk);
+        if (tid == 0) kpad[cur ^ 1] = any != 0ull;
+      }
     }
     __syncthreads();
   }
@@ -366,7 +410,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[gq][dt][r] * inv);
       *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
     }
-    if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_run[gq] * c + log2f(l)) * LN2_F : INFINITY;
+    if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_ref[gq] + log2f(l)) * LN2_F : INFINITY;
   }
 }
 
@@ -478,6 +522,14 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   if (t0 < n_qt) { load(t0); store(0, t0); }
   __syncthreads();
   smer_vm_drain();  // prologue loads retired before the loop (common.h)
+  // K pre-scaled by c = scale * log2(e) and the S chain seeded with -lse
+  // (log2 units): p = 2^acc leaves the MFMA with no per-score arithmetic
+#pragma unroll
+  for (int gk = 0; gk < KG; ++gk)
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kf[gk][s][e] = (bf16)((float)kf[gk][s][e] * c);
   for (int t = t0; t < n_qt; ++t) {
     const int cur = (t - t0) & 1;
     const bool more = t + 1 < n_qt;
@@ -494,13 +546,13 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       const int k16 = (k0w + gk * 16) >> 4;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f}, dpacc = sacc;
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
+        f32x4 sacc = -l4, dpacc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < C::NS; ++s) {
           sacc = mfma16(row_frag<D>(Qs, mt * 16, s, lane), kf[gk][s], sacc);
           dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[gk][s], dpacc);
         }
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&s_lse[cur][mt * 16 + 4 * g]);
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
         // forward lane (G, c) of word [q16][key tile] holds (query c, key
         // 16*mk + 4G + R) at bit 4R + mk: this lane (key c16 of 16-block k16,
@@ -515,7 +567,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float pv = fast_exp2(fmaf(sacc[r], c, -l4[r]));
+          float pv = fast_exp2(sacc[r]);
           if (CAUSAL && diag && kj > t * KVB + mt * 16 + 4 * g + r) pv = 0.f;
           float dpv = dpacc[r];
           float pdv = pv;
@@ -593,6 +645,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
+  __shared__ int kpad[2];  // the staged tile has a padded / out-of-range key
   // forward's keep words: [query 16-block of the block][lane] for the
   // staged key tile (16 bits each, the forward's own lane mapping)
   __shared__ __attribute__((aligned(16))) uint16_t s_msk[2][4 * QG][64];
@@ -654,7 +707,12 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
-    if (tid < KVB) kbias[0][tid] = key_bias(tid);
+    if (tid < KVB) {  // wave 0
+      const float kbz = key_bias(tid);
+      kbias[0][tid] = kbz;
+      const uint64_t any = __ballot(kbz != 0.f);
+      if (tid == 0) kpad[0] = any != 0ull;
+    }
     if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[0][0][0])[tid] = mask_load(0, tid);
   }
 #pragma unroll
@@ -683,6 +741,17 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   }
   __syncthreads();
   smer_vm_drain();  // prologue loads retired before the loop (common.h)
+  // Q pre-scaled by c = scale * log2(e) (the forward's rounding, bit for
+  // bit) and the S chain seeded with -lse: p = 2^acc
+  f32x4 negl[QG];
+#pragma unroll
+  for (int gq = 0; gq < QG; ++gq) {
+    negl[gq] = f32x4{-lse2[gq], -lse2[gq], -lse2[gq], -lse2[gq]};
+#pragma unroll
+    for (int s = 0; s < C::NS; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[gq][s][e] = (bf16)((float)qf[gq][s][e] * c);
+  }
   for (int t = 0; t < n_tiles; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
@@ -699,10 +768,9 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     f32x4 sacc[QG][4], dpacc[QG][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
 #pragma unroll
       for (int gq = 0; gq < QG; ++gq) {
-        sacc[gq][mt] = kbv;
+        sacc[gq][mt] = negl[gq];
         dpacc[gq][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
@@ -714,6 +782,15 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
           sacc[gq][mt] = mfma16(kf, qf[gq][s], sacc[gq][mt]);
           dpacc[gq][mt] = mfma16(vfr, of[gq][s], dpacc[gq][mt]);
         }
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(kpad[cur])) {
+      // -inf on padded / out-of-range keys (tiles without any skip this)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f32x4 kbv = *reinterpret_cast<const f32x4*>(&kbias[cur][mt * 16 + 4 * g]);
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) sacc[gq][mt] += kbv;
       }
     }
     bf16x8 sf[QG][2];
@@ -739,7 +816,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float pv = fast_exp2(fmaf(sacc[gq][mt][r], c, -lse2[gq]));
+          float pv = fast_exp2(sacc[gq][mt][r]);
           if (CAUSAL && diag && t * KVB + mt * 16 + 4 * g + r > qi) pv = 0.f;
           // dS = P (keep * dP / (1 - p) - delta)
           ds[mt][r] = pv * fmaf(dpv[r], DROP ? drop_scale : 1.f, -dlt[gq]);
@@ -761,7 +838,12 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
       asm volatile("" : "+v"(npad));  // keeps the compare (and its wait) here
-      if (tid < KVB) kbias[cur ^ 1][tid] = ((t + 1) * KVB + tid >= Lk || npad) ? -INFINITY : 0.f;
+      if (tid < KVB) {  // wave 0
+        const bool pk = (t + 1) * KVB + tid >= Lk || npad;
+        kbias[cur ^ 1][tid] = pk ? -INFINITY : 0.f;
+        const uint64_t any = __ballot(pk);
+        if (tid == 0) kpad[cur ^ 1] = any != 0ull;
+      }
       if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[cur ^ 1][0][0])[tid] = nmask;
     }
     __syncthreads();

@@ -289,6 +289,72 @@ def test_attention_padded_keys_with_huge_scores(D):
     assert rel_err(o, ro) < 2e-2
 
 
+def _ramped_keys(q, k, B, H, L, D, ramp, top):
+    """Key norms ramping over the key tiles (see the test below)."""
+    g = torch.linspace(0.2, top, L, device=dev)
+    if ramp == "down":
+        g = g.flip(0)
+    gk = g.view(1, L, 1, 1).expand(B, L, H, 1).clone()
+    if ramp == "mixed":
+        gk[:, :, 1::2] = g.flip(0).view(1, L, 1, 1)
+    return (k.float().view(B, L, H, D) * gk).view(B * L, H * D).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("D", [32, 64])
+@pytest.mark.parametrize("ramp", ["up", "down", "mixed"])
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_deferred_max_rescale(D, ramp, causal):
+    """The bf16 forward keeps a per-query reference max and rescales only
+    when a tile's scores pass it by more than 2^8 (or on a query's first
+    key).  N(0, 1) scores never take that branch after the first tile, so
+    the key norms ramp across the 5 (ragged) key tiles: 'up' raises every
+    query's max tile after tile, 'down' never moves it after the first,
+    'mixed' flips the ramp per head so some rows rescale while their wave
+    neighbours do not.
+    (1) Moderate ramp (scores to ~17 in log2 units): forward and backward
+        against the fp32 reference at the usual bf16 tolerances.
+    (2) Steep ramp (scores to ~70): the forward against fp32 math on the
+        operands the kernel actually multiplies -- Q pre-scaled by
+        scale * log2(e) and rounded to bf16 (one extra rounding of Q, whose
+        effect grows with |score|: 0.1 in lse at these scores) -- so that
+        only the rescale bookkeeping is under test."""
+    O = ops()
+    B, H, L = 2, 4, 300
+    torch.manual_seed(5)
+    q, k0, v, kpm = _attn_inputs(B, H, L, L, D, torch.bfloat16, True)
+    scale = 1.0 / math.sqrt(D)
+    for top, qmul in ((3.0, 1.0), (5.0, 2.0)):
+        k = _ramped_keys(q, k0, B, H, L, D, ramp, top)
+        qq = (q.float() * qmul).to(torch.bfloat16)
+        o = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B, H, L, device=dev)
+        O.attn_fwd(qq, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal, scale=scale)
+        if top == 3.0:
+            qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (qq, k, v))
+            ro, rlse = attn_ref(qf, kf, vf, B, H, L, L, D, kpm, causal, scale)
+            torch.cuda.synchronize()
+            assert rel_err(o, ro) < 2e-2
+            assert (lse - rlse).abs().max().item() < 2e-2
+            do = torch.randn(B * L, H * D, device=dev).to(torch.bfloat16)
+            ro.backward(do.float())
+            dq, dk, dv = torch.empty_like(qq), torch.empty_like(k), torch.empty_like(k)
+            O.attn_bwd(qq, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm,
+                       causal=causal, scale=scale)
+            torch.cuda.synchronize()
+            for a, b in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+                assert rel_err(a, b) < 4e-2
+        else:
+            c32 = torch.tensor(scale, dtype=torch.float32) * torch.tensor(1.4426950408889634,
+                                                                          dtype=torch.float32)
+            qc = (qq.float() * c32.item()).to(torch.bfloat16)
+            q_eff = qc.float() * (math.log(2.0) / scale)
+            ro, rlse = attn_ref(q_eff, k.float(), v.float(), B, H, L, L, D, kpm, causal, scale)
+            torch.cuda.synchronize()
+            assert torch.isfinite(o.float()).all()
+            assert rel_err(o, ro) < 2e-2
+            assert (lse - rlse).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
                                                  (torch.float32, 2, 2, 96, True),
                                                  (torch.bfloat16, 16, 8, 512, False),
