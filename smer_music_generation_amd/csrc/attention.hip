@@ -316,7 +316,9 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
         const float m_new = fmaxf(m_run[gq], gmax);
         const float ref = m_new == -INFINITY ? m_ref[gq] : m_new;
         const float d = ref - m_ref[gq];
-        const float alpha = fast_exp2(-d);
+        // nothing accumulated yet (l = acc = 0): a first max far below the
+        // initial reference would overflow 2^-d, and 0 * inf is NaN
+        const float alpha = m_run[gq] == -INFINITY ? 0.f : fast_exp2(-d);
         l_run[gq] *= alpha;
 #pragma unroll
         for (int i = 0; i < C::NDT; ++i) acc[gq][i] *= alpha;

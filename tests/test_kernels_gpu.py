@@ -355,6 +355,41 @@ def test_attention_deferred_max_rescale(D, ramp, causal):
             assert (lse - rlse).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("causal", [False, True])
+def test_attention_first_keys_far_below(causal):
+    """Every query's first key tile scores far below zero (|s| * log2(e) of
+    several hundred, as large un-normalised activations give) and later
+    tiles above it: the first reference max then sits far below the
+    initial one, and nothing may overflow on the way (no NaN / inf)."""
+    O = ops()
+    B, H, L, D = 2, 2, 200, 64
+    torch.manual_seed(11)
+    u = torch.randn(1, H * D, device=dev)
+    q = (u * 6.0 + torch.randn(B * L, H * D, device=dev)).to(torch.bfloat16)
+    k = torch.randn(B * L, H * D, device=dev)
+    kv = k.view(B, L, H * D)
+    kv[:, :64] = -u * 6.0 + 0.5 * kv[:, :64]
+    k = k.to(torch.bfloat16)
+    v = torch.randn(B * L, H * D, device=dev).to(torch.bfloat16)
+    scale = 0.125
+    o = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, causal=causal, scale=scale)
+    c32 = torch.tensor(scale, dtype=torch.float32) * torch.tensor(1.4426950408889634, dtype=torch.float32)
+    q_eff = (q.float() * c32.item()).to(torch.bfloat16).float() * (math.log(2.0) / scale)
+    ro, rlse = attn_ref(q_eff, k.float(), v.float(), B, H, L, L, D, None, causal, scale)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o.float()).all() and torch.isfinite(lse).all()
+    assert rel_err(o, ro) < 2e-2
+    assert (lse - rlse).abs().max().item() < 2e-2
+    do = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(k)
+    O.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, causal=causal, scale=scale)
+    torch.cuda.synchronize()
+    for t in (dq, dk, dv):
+        assert torch.isfinite(t.float()).all()
+
+
 @pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
                                                  (torch.float32, 2, 2, 96, True),
                                                  (torch.bfloat16, 16, 8, 512, False),
