@@ -135,6 +135,18 @@ int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D,
                   void* dq, long lddq, void* dk, long lddk, void* dv, long lddv,
                   void* workspace, size_t ws_bytes, const void* drop_mask,
                   smer_stream_t stream);
+/* smer_attn_bwd (bf16) that also writes e4m3 copies e4m3(g * qs[0]) of dQ
+ * (dq8, nullable) and of dK / dV (dk8 and dv8 together, nullable) beside the
+ * bf16 gradients, folding max|g| into *amax (float bits, atomicMax): the fp8
+ * input of the QKV / cross-Q dgrads in the C4 fp8 step (transformer.py:389,
+ * 459 differentiated by train.py:783).  Copies 4-B aligned, strides % 4. */
+int smer_attn_bwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
+                      const void* k, long ldk, const void* v, long ldv, const void* o, long ldo,
+                      const void* dout, long lddo, const float* lse, const uint8_t* kpm,
+                      int causal, float scale, float drop_p, uint32_t seed, void* dq, long lddq,
+                      void* dk, long lddk, void* dv, long lddv, void* workspace, size_t ws_bytes,
+                      const void* drop_mask, void* dq8, long lddq8, void* dk8, long lddk8,
+                      void* dv8, long lddv8, const float* qs, unsigned* amax, smer_stream_t stream);
 /* out fp32 [B, Lq, Lk] = mean over heads of the attention probabilities. */
 int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
                       const void* q, long ldq, const void* k, long ldk, const float* lse,

@@ -35,6 +35,10 @@ SIGNATURES = {
     "smer_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P,
                               c_long, P, c_long, P, c_long, P, P, c_int, c_float, c_float, c_u32,
                               P, c_long, P, c_long, P, c_long, P, c_size, P, P]),
+    "smer_attn_bwd_fp8": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
+                                  P, c_long, P, c_long, P, P, c_int, c_float, c_float, c_u32, P, c_long,
+                                  P, c_long, P, c_long, P, c_size, P, P, c_long, P, c_long, P, c_long,
+                                  P, P, P]),
     "smer_attn_weights": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long,
                                   P, P, c_int, c_float, P, P]),
     "smer_attn_decode": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, P, c_long, c_long,

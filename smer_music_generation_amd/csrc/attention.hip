@@ -423,6 +423,19 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
 // read from LDS per query tile feed KG groups.
 // CAUSAL: the causal instances carry the per-element key > query test on
 // diagonal tiles; the non-causal ones (encoder, cross-attention) none.
+// e4m3 copies e4m3(g * qs) of the backward's bf16 outputs (the next dgrad's
+// fp8 input, C4), max|g| folded into amax; a null pointer: no copy
+struct AttnQ8 {
+  uint8_t* dq;
+  long lddq;
+  uint8_t* dk;
+  long lddk;
+  uint8_t* dv;
+  long lddv;
+  const float* qs;
+  unsigned* amax;
+};
+
 template <int D, bool DROP, int KG, bool MSK, bool CAUSAL>
 __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
@@ -430,7 +443,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
     uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dk, long lddk,
-    bf16* __restrict__ dv, long lddv, const uint64_t* __restrict__ drop_mask) {
+    bf16* __restrict__ dv, long lddv, const uint64_t* __restrict__ drop_mask, AttnQ8 q8) {
   using C = AttnCfg<D>;
   constexpr int KB = 64 * KG;  // keys per block
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
@@ -610,6 +623,9 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     if (more) store(cur ^ 1, t + 1);
     __syncthreads();
   }
+  const bool w8 = q8.dk != nullptr;  // (then dv too)
+  const float q8s = w8 ? *q8.qs : 1.f;
+  float am = 0.f;
 #pragma unroll
   for (int gk = 0; gk < KG; ++gk) {
     const int kj = k0w + gk * 16 + c16;
@@ -627,8 +643,21 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       }
       *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
       *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
+      if (w8) {  // e4m3 copies of the stored (bf16-rounded) values
+        float fk[4], fv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          fk[r] = (float)wk[r];
+          fv[r] = (float)wv[r];
+        }
+        const long col = h * D + dt * 16 + 4 * g;
+        *reinterpret_cast<uint32_t*>(q8.dk + (long)(b * Lk + kj) * q8.lddk + col) = smer_q8x4(fk, q8s);
+        *reinterpret_cast<uint32_t*>(q8.dv + (long)(b * Lk + kj) * q8.lddv + col) = smer_q8x4(fv, q8s);
+        am = fmaxf(am, fmaxf(smer_absmax4(fk), smer_absmax4(fv)));
+      }
     }
   }
+  if (w8) smer_amax_commit(q8.amax, am);
 }
 
 // ---------------------------------------------------------------------------
@@ -641,7 +670,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     const bf16* __restrict__ dout, long lddo, const float* __restrict__ lse,
     float* __restrict__ delta, const uint8_t* __restrict__ kpm, int causal, float scale,
     uint32_t drop_thr, uint32_t seed, float drop_scale, bf16* __restrict__ dq, long lddq,
-    const uint64_t* __restrict__ drop_mask, const bf16* __restrict__ o, long ldo) {
+    const uint64_t* __restrict__ drop_mask, const bf16* __restrict__ o, long ldo, AttnQ8 q8) {
   using C = AttnCfg<D>;
   constexpr int QB = 64 * QG;  // queries per block
   const int nq16 = (Lq + 15) >> 4, nkt = (Lk + KVB - 1) / KVB;
@@ -850,6 +879,9 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     }
     __syncthreads();
   }
+  const bool w8 = q8.dq != nullptr;
+  const float q8s = w8 ? *q8.qs : 1.f;
+  float am = 0.f;
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     const int qi = q0w + gq * 16 + c16;
@@ -861,8 +893,17 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(adq[gq][dt][r] * scale);
       *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;
+      if (w8) {  // e4m3 copy of the stored (bf16-rounded) values
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = (float)w[r];
+        *reinterpret_cast<uint32_t*>(q8.dq + (long)(b * Lq + qi) * q8.lddq + h * D + dt * 16 + 4 * g) =
+            smer_q8x4(f, q8s);
+        am = fmaxf(am, smer_absmax4(f));
+      }
     }
   }
+  if (w8) smer_amax_commit(q8.amax, am);
 }
 
 template <typename T>
@@ -1546,7 +1587,8 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                             const float* lse, float* delta, const uint8_t* kpm, int causal,
                             float scale, uint32_t thr, uint32_t seed, float ds, void* dq,
                             long lddq, void* dk, long lddk, void* dv, long lddv,
-                            const uint64_t* mask, const void* o, long ldo, hipStream_t s) {
+                            const uint64_t* mask, const void* o, long ldo, const AttnQ8& q8,
+                            hipStream_t s) {
   if (!thr) mask = nullptr;
   // two key groups per wave once there are enough blocks to fill the chip
   const bool kg2 = (long)((Lk + 127) / 128) * B * H >= 512 && D <= 64;
@@ -1567,23 +1609,23 @@ static void bwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
     hipLaunchKernelGGL(kdq, dim3(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H), dim3(256), 0, s, B, H,
                        Lq, Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                        (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
-                       (bf16*)dq, lddq, mask, (const bf16*)o, ldo);
+                       (bf16*)dq, lddq, mask, (const bf16*)o, ldo, q8);
   };
   if (o) launch_dq();
   hipLaunchKernelGGL(kdkdv, dim3(kg2 ? (Lk + 127) / 128 : (Lk + 63) / 64, B * H), dim3(256), 0, s, B, H, Lq,
                      Lk, (const bf16*)q, ldq, (const bf16*)k, ldk, (const bf16*)v, ldv,
                      (const bf16*)dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds,
-                     (bf16*)dk, lddk, (bf16*)dv, lddv, mask);
+                     (bf16*)dk, lddk, (bf16*)dv, lddv, mask, q8);
   if (!o) launch_dq();
 }
 
-extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
-                             long ldq, const void* k, long ldk, const void* v, long ldv,
-                             const void* o, long ldo, const void* dout, long lddo,
-                             const float* lse, const uint8_t* kpm, int causal, float scale,
-                             float drop_p, uint32_t seed, void* dq, long lddq, void* dk, long lddk,
-                             void* dv, long lddv, void* workspace, size_t ws_bytes,
-                             const void* drop_mask, smer_stream_t stream) {
+static int attn_bwd_impl(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                         long ldq, const void* k, long ldk, const void* v, long ldv,
+                         const void* o, long ldo, const void* dout, long lddo,
+                         const float* lse, const uint8_t* kpm, int causal, float scale,
+                         float drop_p, uint32_t seed, void* dq, long lddq, void* dk, long lddk,
+                         void* dv, long lddv, void* workspace, size_t ws_bytes,
+                         const void* drop_mask, const AttnQ8& q8, smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && D > 0, "smer_attn_bwd: bad sizes");
   SMER_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "smer_attn_bwd: null pointer");
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
@@ -1599,9 +1641,9 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
     // SMER_DQ_DELTA=0 (A/B builds): separate delta pass, dK / dV kernel first
     const void* of = SMER_DQ_DELTA ? o : nullptr;
     if (!of) launch_delta<bf16>(B, H, Lq, D, o, ldo, dout, lddo, delta, s);
-    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
-    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
-    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, s);
+    if (D == 32) bwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, q8, s);
+    else if (D == 64) bwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, q8, s);
+    else if (D == 128) bwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, dout, lddo, lse, delta, kpm, causal, scale, thr, seed, ds, dq, lddq, dk, lddk, dv, lddv, (const uint64_t*)drop_mask, of, ldo, q8, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_bwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     hipLaunchKernelGGL(attn_delta_scalar<float>, dim3((nrow + 255) / 256), dim3(256), 0, s, B, H,
@@ -1626,6 +1668,38 @@ extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   }
   SMER_CHECK_LAUNCH("smer_attn_bwd");
   return SMER_OK;
+}
+
+extern "C" int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                             long ldq, const void* k, long ldk, const void* v, long ldv,
+                             const void* o, long ldo, const void* dout, long lddo,
+                             const float* lse, const uint8_t* kpm, int causal, float scale,
+                             float drop_p, uint32_t seed, void* dq, long lddq, void* dk, long lddk,
+                             void* dv, long lddv, void* workspace, size_t ws_bytes,
+                             const void* drop_mask, smer_stream_t stream) {
+  const AttnQ8 none{};
+  return attn_bwd_impl(dtype, B, H, Lq, Lk, D, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, kpm,
+                       causal, scale, drop_p, seed, dq, lddq, dk, lddk, dv, lddv, workspace, ws_bytes,
+                       drop_mask, none, stream);
+}
+
+extern "C" int smer_attn_bwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
+                                 const void* k, long ldk, const void* v, long ldv, const void* o,
+                                 long ldo, const void* dout, long lddo, const float* lse,
+                                 const uint8_t* kpm, int causal, float scale, float drop_p,
+                                 uint32_t seed, void* dq, long lddq, void* dk, long lddk, void* dv,
+                                 long lddv, void* workspace, size_t ws_bytes, const void* drop_mask,
+                                 void* dq8, long lddq8, void* dk8, long lddk8, void* dv8, long lddv8,
+                                 const float* qs, unsigned* amax, smer_stream_t stream) {
+  SMER_REQUIRE(!dk8 == !dv8, "smer_attn_bwd_fp8: dK and dV copies go together");
+  SMER_REQUIRE((!dq8 && !dk8) || (qs && amax), "smer_attn_bwd_fp8: scale and amax");
+  auto al4 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 3) == 0 && ld % 4 == 0); };
+  SMER_REQUIRE(al4(dq8, lddq8) && al4(dk8, lddk8) && al4(dv8, lddv8),
+               "smer_attn_bwd_fp8: 4-B aligned copies and row strides");
+  const AttnQ8 q8{(uint8_t*)dq8, lddq8, (uint8_t*)dk8, lddk8, (uint8_t*)dv8, lddv8, qs, amax};
+  return attn_bwd_impl(SMER_BF16, B, H, Lq, Lk, D, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse,
+                       kpm, causal, scale, drop_p, seed, dq, lddq, dk, lddk, dv, lddv, workspace,
+                       ws_bytes, drop_mask, q8, stream);
 }
 
 extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,

@@ -339,6 +339,24 @@ __device__ __forceinline__ uint2 smer_q8x8(const float (&v)[8], float qs) {
   }
   return make_uint2(w[0], w[1]);
 }
+// 4 values -> 4 e4m3 bytes (little-endian in one word), as smer_q8x8
+__device__ __forceinline__ uint32_t smer_q8x4(const float (&v)[4], float qs) {
+  float f[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float x = v[k] * qs;
+    f[k] = x == x ? fminf(fmaxf(x, -448.f), 448.f) : x;
+  }
+  int p = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  p = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], p, true);
+  return (uint32_t)p;
+}
+__device__ __forceinline__ float smer_absmax4(const float (&v)[4]) {
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m = fmaxf(m, v[k] == v[k] ? fabsf(v[k]) : __builtin_inff());
+  return m;
+}
 __device__ __forceinline__ float smer_absmax8(const float (&v)[8]) {
   // NaN maps to +inf (fmaxf would drop it): the amax slot then reports the
   // non-finite activation (Fp8Forward.finite) and the next scale falls back to 1

@@ -435,7 +435,7 @@ class Engine:
         G = self.grad_views()
         Mt, Ms = B * T, B * S
 
-        from .fp8 import FP8_DGRAD, eligible
+        from .fp8 import FP8_ATTN_DGRAD, FP8_DGRAD, eligible
         f8 = ctx.f8 if FP8_DGRAD else None
 
         def ln_bwd(g_in, y_, mu, rs, wb, dx_, dxd_, seed_, gw, site):
@@ -452,6 +452,20 @@ class Engine:
             ops.layernorm_bwd(g_in, y_, mu, rs, wb[0], dx_, q8=q, qs=f8.qs_of(si), amax=f8.amax_of(si), **kw)
             f8.record_bwd(site)
             return (q, si) if site in f8.bwd_ready else None
+
+        def attn_q8(shape, site, parts):
+            """e4m3 copy buffer of an attention-backward gradient [rows, cols]
+            and the q8 argument of ops.attn_bwd; parts: column slices (dq, dk,
+            dv) of the copy, None for a gradient without one.  Returns
+            (q8 arg, gq for dgrad or None)."""
+            if f8 is None or not FP8_ATTN_DGRAD:
+                return None, None
+            si = f8.site(site)
+            buf = torch.empty(shape, dtype=torch.uint8, device=dev)
+            views = [None if p is None else buf[:, p[0]:p[1]] for p in parts]
+            f8.record_bwd(site)
+            return (views[0], views[1], views[2], f8.qs_of(si), f8.amax_of(si)), \
+                ((buf, si) if site in f8.bwd_ready else None)
 
         def dgrad(gq, g, wname, w, q_site=None, **epi):
             """g @ w; on the fp8 MFMA (e4m3(g) . e4m3(w^T)^T) when g has a usable
@@ -510,12 +524,14 @@ class Engine:
             doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
+            q8c, dqcq = attn_q8((Mt, d), "b.dec%d.dqc" % i, [(0, d), None, None])
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
-                         drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)))
+                         drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)),
+                         q8=q8c)
             wg(dqc, x1, GL.cq_w, db=GL.cq_b)
             wg(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
-            dx1 = ops.linear_dgrad(dqc, L.cq_w, residual=dy2)
+            dx1, _ = dgrad(dqcq, dqc, "dec%d.cq" % i, L.cq_w, residual=dy2)
             # self-attention block
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
@@ -523,12 +539,13 @@ class Engine:
             wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             do, _ = dgrad(dy1q, dy1d, "dec%d.sao" % i, L.sa_ow)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
+            q8s, dqkvq = attn_q8((Mt, 3 * d), "b.dec%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
-                         seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)))
+                         seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)), q8=q8s)
             wg(dqkv, y_in, GL.sa_w, db=GL.sa_b)
-            dy = ops.linear_dgrad(dqkv, L.sa_w, residual=dy1)
+            dy, _ = dgrad(dqkvq, dqkv, "dec%d.sa" % i, L.sa_w, residual=dy1)
             if hook:
                 self._join(side)
                 hook("dec%d" % i)
@@ -559,12 +576,13 @@ class Engine:
             wg(dy1d, o, GL.out_w, db=GL.out_b)
             do, _ = dgrad(dy1q, dy1d, "enc%d.out" % i, L.out_w)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
+            q8s, dqkvq = attn_q8((Ms, 3 * d), "b.enc%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
-                         seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)))
+                         seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)), q8=q8s)
             wg(dqkv, x_in, GL.in_w, db=GL.in_b)
-            dx = ops.linear_dgrad(dqkv, L.in_w, residual=dy1)
+            dx, _ = dgrad(dqkvq, dqkv, "enc%d.in" % i, L.in_w, residual=dy1)
             if hook:
                 self._join(side)
                 hook("enc%d" % i)

@@ -11,16 +11,17 @@ stacked cross-attention K/V of the memory (`transformer.py:389,393,459,463,
 working weights bf16.
 
 Backward (FP8_DGRAD): the dgrad products whose input gradient comes from a
-LayerNorm backward or from the FFN2 dgrad run as e4m3(dY) . e4m3(W^T)^T on
-the same kernel: FFN2 dgrad (ReLU gate in the epilogue, writing the e4m3
-copy of dh), FFN1 dgrad (residual) and the attention out-projection dgrads.
-The LayerNorm backward writes the gradient's e4m3 copy beside its bf16
-output; scales are delayed like the forward's (the amax recorded in step
-t - 1), so a backward site switches to fp8 once it has one step of
-history (the first step's backward is bf16).  W^T copies are quantised with
-the forward copies, once per optimizer step.  QKV / cross-Q dgrads (input:
-the attention backward), the memory dgrad and every weight gradient stay
-bf16.
+LayerNorm backward, the FFN2 dgrad or the attention backward run as
+e4m3(dY) . e4m3(W^T)^T on the same kernel: FFN2 dgrad (ReLU gate in the
+epilogue, writing the e4m3 copy of dh), FFN1 dgrad (residual), the attention
+out-projection dgrads, and the QKV / cross-Q dgrads (the attention
+backward kernels write dQ / dK / dV's e4m3 copies, round 3).  Producers
+write the gradient's e4m3 copy beside its bf16 output; scales are delayed
+like the forward's (the amax recorded in step t - 1), so a backward site
+switches to fp8 once it has one step of history (the first step's backward
+is bf16).  W^T copies are quantised with the forward copies, once per
+optimizer step.  The memory dgrad (K = 12 * 2d) and every weight gradient
+stay bf16.
 
 Scaling (no standalone quantise pass over activations):
   * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy
@@ -45,6 +46,9 @@ from . import ops
 N_SITES = 512
 # fp8 backward dgrads (SMER_FP8_DGRAD=0: bf16 backward, A/B and tests)
 FP8_DGRAD = os.environ.get("SMER_FP8_DGRAD", "1") != "0"
+# ... including the QKV / cross-Q dgrads fed by the attention backward
+# (SMER_FP8_ATTN_DGRAD=0: those stay bf16, A/B)
+FP8_ATTN_DGRAD = os.environ.get("SMER_FP8_ATTN_DGRAD", "1") != "0"
 
 
 class Fp8Forward:
@@ -113,10 +117,11 @@ class Fp8Forward:
         MFMA (as e4m3(dY) . e4m3(W^T)^T)."""
         out = []
         for i, L in enumerate(W.enc):
-            out += [("enc%d.out" % i, L.out_w), ("enc%d.l1" % i, L.l1_w), ("enc%d.l2" % i, L.l2_w)]
+            out += [("enc%d.in" % i, L.in_w), ("enc%d.out" % i, L.out_w), ("enc%d.l1" % i, L.l1_w),
+                    ("enc%d.l2" % i, L.l2_w)]
         for i, L in enumerate(W.dec):
-            out += [("dec%d.sao" % i, L.sa_ow), ("dec%d.cao" % i, L.ca_ow), ("dec%d.l1" % i, L.l1_w),
-                    ("dec%d.l2" % i, L.l2_w)]
+            out += [("dec%d.sa" % i, L.sa_w), ("dec%d.sao" % i, L.sa_ow), ("dec%d.cq" % i, L.cq_w),
+                    ("dec%d.cao" % i, L.ca_ow), ("dec%d.l1" % i, L.l1_w), ("dec%d.l2" % i, L.l2_w)]
         return out
 
     def _quantize_weights_t(self, W):

@@ -390,6 +390,39 @@ def test_attention_first_keys_far_below(causal):
         assert torch.isfinite(t.float()).all()
 
 
+@pytest.mark.parametrize("kg2", [False, True])
+def test_attention_bwd_e4m3_copies(kg2):
+    """smer_attn_bwd_fp8: the bf16 gradients are the plain backward's bit for
+    bit, the e4m3 copies are e4m3(g * qs) of them (nearest-even, saturated),
+    and amax holds max|g| over the three gradients (float bits)."""
+    O = ops()
+    B, H, L, D = (16, 8, 512, 64) if kg2 else (2, 3, 200, 64)
+    q, k, v, kpm = _attn_inputs(B, H, L, L, D, torch.bfloat16, True)
+    o = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=dev)
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, scale=0.125)
+    do = torch.randn_like(o)
+    ref = [torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16) for _ in range(3)]
+    O.attn_bwd(q, k, v, o, do, lse, *ref, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, scale=0.125,
+               drop_p=0.1, seed=5)
+    got = torch.empty(B * L, 3 * H * D, device=dev, dtype=torch.bfloat16)
+    q8 = torch.zeros(B * L, 3 * H * D, device=dev, dtype=torch.uint8)
+    qs = torch.tensor([37.0], device=dev)
+    amax = torch.zeros(1, dtype=torch.int32, device=dev)
+    hd = H * D
+    O.attn_bwd(q, k, v, o, do, lse, got[:, :hd], got[:, hd:2 * hd], got[:, 2 * hd:], B=B, H=H, Lq=L,
+               Lk=L, D=D, kpm=kpm, scale=0.125, drop_p=0.1, seed=5,
+               q8=(q8[:, :hd], q8[:, hd:2 * hd], q8[:, 2 * hd:], qs, amax))
+    torch.cuda.synchronize()
+    for j in range(3):
+        g = got[:, j * hd:(j + 1) * hd]
+        assert torch.equal(g, ref[j])
+        want = (g.float() * 37.0).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q8[:, j * hd:(j + 1) * hd], want)
+    m = max(t.float().abs().max().item() for t in ref)
+    assert amax.view(torch.float32).item() == m
+
+
 @pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
                                                  (torch.float32, 2, 2, 96, True),
                                                  (torch.bfloat16, 16, 8, 512, False),
