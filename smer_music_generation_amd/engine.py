@@ -503,6 +503,11 @@ class Engine:
         # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
         # one dgrad GEMM (K = L*2d) after the decoder loop gives dmemory
         dkvc_all = torch.empty(Ms, self.n_dec * 2 * d, dtype=dt, device=dev)
+        # fp8: one e4m3 copy of it (and of each layer's cross dQ) under one
+        # scale site, so the memory dgrad runs on the fp8 MFMA as well
+        cross8 = None
+        if f8 is not None and FP8_ATTN_DGRAD and self.n_dec:
+            cross8 = (f8.site("b.cross"), torch.empty(Ms, self.n_dec * 2 * d, dtype=torch.uint8, device=dev))
         for i in reversed(range(self.n_dec)):
             L, GL = W.dec[i], G.dec[i]
             (y_in, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2, h, y3, m3,
@@ -524,7 +529,14 @@ class Engine:
             doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
-            q8c, dqcq = attn_q8((Mt, d), "b.dec%d.dqc" % i, [(0, d), None, None])
+            q8c, dqcq = None, None
+            if cross8 is not None:
+                si, dkvc8 = cross8
+                dqc8 = torch.empty(Mt, d, dtype=torch.uint8, device=dev)
+                q8c = (dqc8, dkvc8[:, i * 2 * d:i * 2 * d + d], dkvc8[:, i * 2 * d + d:(i + 1) * 2 * d],
+                       f8.qs_of(si), f8.amax_of(si))
+                f8.record_bwd("b.cross")
+                dqcq = (dqc8, si) if "b.cross" in f8.bwd_ready else None
             ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)),
@@ -551,7 +563,11 @@ class Engine:
                 hook("dec%d" % i)
         d_tgt = dy
         if self.n_dec:
-            dmem = ops.linear_dgrad(dkvc_all, W.ckv_all, out_f32=torch.empty(Ms, d, device=dev))
+            if (cross8 is not None and "b.cross" in f8.bwd_ready and f8.weight_t("ckv") is not None
+                    and eligible(Ms, d, self.n_dec * 2 * d)):
+                dmem, _ = dgrad((cross8[1], cross8[0]), dkvc_all, "ckv", W.ckv_all)
+            else:
+                dmem = ops.linear_dgrad(dkvc_all, W.ckv_all, out_f32=torch.empty(Ms, d, device=dev))
         else:
             dmem = torch.zeros(Ms, d, device=dev)
         # encoder

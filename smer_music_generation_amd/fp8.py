@@ -20,8 +20,9 @@ write the gradient's e4m3 copy beside its bf16 output; scales are delayed
 like the forward's (the amax recorded in step t - 1), so a backward site
 switches to fp8 once it has one step of history (the first step's backward
 is bf16).  W^T copies are quantised with the forward copies, once per
-optimizer step.  The memory dgrad (K = 12 * 2d) and every weight gradient
-stay bf16.
+optimizer step.  The memory dgrad (K = 12 * 2d) reads one e4m3 copy of
+every layer's cross-attention dK | dV under a single scale site (shared with
+the cross dQ copies).  Every weight gradient stays bf16.
 
 Scaling (no standalone quantise pass over activations):
   * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy
@@ -122,6 +123,8 @@ class Fp8Forward:
         for i, L in enumerate(W.dec):
             out += [("dec%d.sa" % i, L.sa_w), ("dec%d.sao" % i, L.sa_ow), ("dec%d.cq" % i, L.cq_w),
                     ("dec%d.cao" % i, L.ca_ow), ("dec%d.l1" % i, L.l1_w), ("dec%d.l2" % i, L.l2_w)]
+        if getattr(W, "ckv_all", None) is not None:
+            out.append(("ckv", W.ckv_all))
         return out
 
     def _quantize_weights_t(self, W):
