@@ -147,6 +147,15 @@ int smer_attn_bwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long l
                       void* dk, long lddk, void* dv, long lddv, void* workspace, size_t ws_bytes,
                       const void* drop_mask, void* dq8, long lddq8, void* dk8, long lddk8,
                       void* dv8, long lddv8, const float* qs, unsigned* amax, smer_stream_t stream);
+/* smer_attn_fwd (bf16) that also writes the output's e4m3 copy
+ * e4m3(o * qs[0]) (4-B aligned, ldo8 % 4 == 0), max|o| folded into *amax:
+ * the fp8 input of the attention out-projection in the C4 fp8 forward
+ * (transformer.py:389 -> 390/463 -> 464 out_proj).  Head dim 64, drop_mask_in 0. */
+int smer_attn_fwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long ldq, const void* k,
+                      long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
+                      const uint8_t* kpm, int causal, float scale, float drop_p, uint32_t seed,
+                      void* drop_mask, int drop_mask_in, void* o8, long ldo8, const float* qs,
+                      unsigned* amax, smer_stream_t stream);
 /* out fp32 [B, Lq, Lk] = mean over heads of the attention probabilities. */
 int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
                       const void* q, long ldq, const void* k, long ldk, const float* lse,

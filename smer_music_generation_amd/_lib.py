@@ -29,6 +29,9 @@ SIGNATURES = {
                                      c_int, P, c_int, P, c_size, P]),
     "smer_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P,
                               c_long, P, c_long, P, P, c_int, c_float, c_float, c_u32, P, c_int, P]),
+    "smer_attn_fwd_fp8": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
+                                  P, c_long, P, P, c_int, c_float, c_float, c_u32, P, c_int, P, c_long,
+                                  P, P, P]),
     "smer_attn_drop_mask_gen": (c_int, [c_int, c_int, c_int, c_int, c_float, c_u32, P, P]),
     "smer_attn_drop_mask_bytes": (c_size, [c_int, c_int, c_int, c_int]),
     "smer_attn_bwd_workspace": (c_size, [c_int, c_int, c_int, c_int, c_int]),

@@ -138,6 +138,20 @@ __device__ __forceinline__ uint32_t attn_fold_keep(uint32_t acc) {
 // ---------------------------------------------------------------------------
 // bf16 forward
 // ---------------------------------------------------------------------------
+// e4m3 copies e4m3(g * qs) of bf16 attention outputs, max|g| folded into
+// amax (C4 fp8: the next GEMM's input); a null pointer: no copy.  Backward:
+// dQ / dK / dV; forward: O in the dq slot
+struct AttnQ8 {
+  uint8_t* dq;
+  long lddq;
+  uint8_t* dk;
+  long lddk;
+  uint8_t* dv;
+  long lddv;
+  const float* qs;
+  unsigned* amax;
+};
+
 // QG query groups of 16 per wave (block = 64*QG queries): K / V fragments
 // read from LDS once per wave feed QG groups, halving LDS traffic per MFMA
 // at QG = 2 (the forward is otherwise LDS-bandwidth co-limited).
@@ -147,7 +161,9 @@ __device__ __forceinline__ uint32_t attn_fold_keep(uint32_t acc) {
 // Dropout (DROP): per lane and key tile 4 hashes (one per quad of keys),
 // SWAR byte compares, AND masks on the packed bf16 P -- about 20 VALU
 // instructions per 16 scores besides the softmax.
-template <int D, int QG, bool DROP, bool MIN = false>
+// Q8: also the e4m3 copy of O (q8.dq; C4 fp8), a separate instance so that
+// the plain forward's code is untouched by it
+template <int D, int QG, bool DROP, bool MIN = false, bool Q8 = false>
 __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(int B, int H, int Lq, int Lk,
                                                      const bf16* __restrict__ q, long ldq,
                                                      const bf16* __restrict__ k, long ldk,
@@ -157,7 +173,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
                                                      const uint8_t* __restrict__ kpm, int causal,
                                                      float scale, uint32_t drop_thr, uint32_t seed,
                                                      float drop_scale,
-                                                     uint64_t* __restrict__ drop_mask) {
+                                                     uint64_t* __restrict__ drop_mask, AttnQ8 q8) {
   // drop_mask: see smer_attn_drop_mask_bytes (16-bit words, one per lane)
   using C = AttnCfg<D>;
   constexpr int QB = 64 * QG;  // queries per block
@@ -397,6 +413,9 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     }
     __syncthreads();
   }
+  constexpr bool w8 = Q8;
+  const float q8s = w8 ? *q8.qs : 1.f;
+  float am = 0.f;
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     const int qi = q0w + gq * 16 + c16;
@@ -411,9 +430,18 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[gq][dt][r] * inv);
       *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
+      if constexpr (Q8) {  // e4m3 copy of the stored (bf16-rounded) values
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = (float)w[r];
+        *reinterpret_cast<uint32_t*>(q8.dq + (long)(b * Lq + qi) * q8.lddq + h * D + dt * 16 + 4 * g) =
+            smer_q8x4(f, q8s);
+        am = fmaxf(am, smer_absmax4(f));
+      }
     }
     if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_ref[gq] + log2f(l)) * LN2_F : INFINITY;
   }
+  if constexpr (Q8) smer_amax_commit(q8.amax, am);
 }
 
 // ---------------------------------------------------------------------------
@@ -423,19 +451,6 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
 // read from LDS per query tile feed KG groups.
 // CAUSAL: the causal instances carry the per-element key > query test on
 // diagonal tiles; the non-causal ones (encoder, cross-attention) none.
-// e4m3 copies e4m3(g * qs) of the backward's bf16 outputs (the next dgrad's
-// fp8 input, C4), max|g| folded into amax; a null pointer: no copy
-struct AttnQ8 {
-  uint8_t* dq;
-  long lddq;
-  uint8_t* dk;
-  long lddk;
-  uint8_t* dv;
-  long lddv;
-  const float* qs;
-  unsigned* amax;
-};
-
 template <int D, bool DROP, int KG, bool MSK, bool CAUSAL>
 __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     int B, int H, int Lq, int Lk, const bf16* __restrict__ q, long ldq,
@@ -1503,7 +1518,8 @@ template <int D>
 static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ldq, const void* k,
                             long ldk, const void* v, long ldv, void* o, long ldo, float* lse,
                             const uint8_t* kpm, int causal, float scale, uint32_t thr,
-                            uint32_t seed, float ds, uint64_t* mask, int mask_in, hipStream_t s) {
+                            uint32_t seed, float ds, uint64_t* mask, int mask_in, const AttnQ8& q8,
+                            hipStream_t s) {
   // two query groups per wave once there are enough blocks to fill the chip
   const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
   dim3 grid(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H);
@@ -1512,9 +1528,14 @@ static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
                           : (thr ? attn_fwd_bf16<D, 2, true> : attn_fwd_bf16<D, 2, false>))
                   : (min_ ? attn_fwd_bf16<D, 1, true, true>
                           : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>));
+  if constexpr (D == 64) {
+    if (q8.dq)  // (the C-ABI rejects a copy with precomputed keep bits)
+      kern = qg2 ? (thr ? attn_fwd_bf16<D, 2, true, false, true> : attn_fwd_bf16<D, 2, false, false, true>)
+                 : (thr ? attn_fwd_bf16<D, 1, true, false, true> : attn_fwd_bf16<D, 1, false, false, true>);
+  }
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
-                     scale, thr, seed, ds, thr ? mask : nullptr);
+                     scale, thr, seed, ds, thr ? mask : nullptr, q8);
 }
 
 // [bh][query 16-block][key 64-tile][64 lanes] 16-bit words: lane (g, c) of
@@ -1537,11 +1558,11 @@ extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_
   return SMER_OK;
 }
 
-extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
-                             long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
-                             long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
-                             float drop_p, uint32_t seed, void* drop_mask, int drop_mask_in,
-                             smer_stream_t stream) {
+static int attn_fwd_impl(int dtype, int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
+                         const void* k, long ldk, const void* v, long ldv, void* o, long ldo,
+                         float* lse, const uint8_t* kpm, int causal, float scale, float drop_p,
+                         uint32_t seed, void* drop_mask, int drop_mask_in, const AttnQ8& q8,
+                         smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq >= 0 && Lk > 0 && D > 0, "smer_attn_fwd: bad sizes");
   SMER_REQUIRE(!drop_mask_in || drop_mask, "smer_attn_fwd: drop_mask_in without a mask");
   SMER_REQUIRE(!drop_mask || (((uintptr_t)drop_mask) & 15) == 0, "smer_attn_fwd: mask alignment");
@@ -1555,9 +1576,9 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
     SMER_REQUIRE(al16(q) && al16(k) && al16(v), "smer_attn_fwd: 16-B alignment");
     SMER_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && ldo % 4 == 0,
                  "smer_attn_fwd: row strides must be multiples of 8");
-    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
-    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
-    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, s);
+    if (D == 32) fwd_bf16_launch<32>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, q8, s);
+    else if (D == 64) fwd_bf16_launch<64>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, q8, s);
+    else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, q8, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
     SMER_REQUIRE((size_t)Lk * 16 <= 160 * 1024, "smer_attn_fwd(f32): Lk too large");
@@ -1570,6 +1591,29 @@ extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, con
   }
   SMER_CHECK_LAUNCH("smer_attn_fwd");
   return SMER_OK;
+}
+
+extern "C" int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* q,
+                             long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
+                             long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
+                             float drop_p, uint32_t seed, void* drop_mask, int drop_mask_in,
+                             smer_stream_t stream) {
+  const AttnQ8 none{};
+  return attn_fwd_impl(dtype, B, H, Lq, Lk, D, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale,
+                       drop_p, seed, drop_mask, drop_mask_in, none, stream);
+}
+
+extern "C" int smer_attn_fwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
+                                 const void* k, long ldk, const void* v, long ldv, void* o, long ldo,
+                                 float* lse, const uint8_t* kpm, int causal, float scale, float drop_p,
+                                 uint32_t seed, void* drop_mask, int drop_mask_in, void* o8, long ldo8,
+                                 const float* qs, unsigned* amax, smer_stream_t stream) {
+  SMER_REQUIRE(o8 && qs && amax && (((uintptr_t)o8) & 3) == 0 && ldo8 % 4 == 0,
+               "smer_attn_fwd_fp8: 4-B aligned copy, scale and amax");
+  SMER_REQUIRE(D == 64 && !drop_mask_in, "smer_attn_fwd_fp8: head dim 64, keep bits hashed in the kernel");
+  const AttnQ8 q8{(uint8_t*)o8, ldo8, nullptr, 0, nullptr, 0, qs, amax};
+  return attn_fwd_impl(SMER_BF16, B, H, Lq, Lk, D, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal,
+                       scale, drop_p, seed, drop_mask, drop_mask_in, q8, stream);
 }
 
 extern "C" size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int Lk) {

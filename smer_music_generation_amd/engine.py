@@ -246,6 +246,17 @@ class Engine:
         ops.layernorm_fp8(x, wb[0], wb[1], y, mean, rstd, q, f8.qs_of(si), f8.amax_of(si))
         return y, mean, rstd, (q, si)
 
+    @staticmethod
+    def _attn_q8(f8, o, site):
+        """fp8 forward: (q8 argument of ops.attn_fwd, (e4m3 copy of o, site))
+        so that the out-projection reads the attention output in e4m3."""
+        from .fp8 import FP8_ATTN_OUT
+        if f8 is None or not FP8_ATTN_OUT:
+            return None, None
+        si = f8.site(site)
+        q = torch.empty(o.shape, dtype=torch.uint8, device=o.device)
+        return (q, f8.qs_of(si), f8.amax_of(si)), (q, si)
+
     def _lin(self, f8, x, xq, wname, w, b, q_site=None, **epi):
         """x @ w^T + epilogue: on the fp8 MFMA when x has an e4m3 copy xq and
         the shape tiles, else bf16.  q_site: also write the e4m3 copy of the
@@ -324,10 +335,12 @@ class Engine:
             qkv = self._lin(f8, x, xq, "enc%d.in" % i, L.in_w, L.in_b)
             o = torch.empty(B * S, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, S, device=dev)
+            q8, oq = self._attn_q8(f8, o, "enc%d.o" % i)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
                          D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)),
-                         drop_mask=amask(("enc", i), S, S))
-            y1 = ops.linear(o, L.out_w, L.out_b, residual=x, drop_p=p_tr, seed=sd(_site("enc", i, 1)))
+                         drop_mask=amask(("enc", i), S, S), q8=q8)
+            y1 = self._lin(f8, o, oq, "enc%d.out" % i, L.out_w, L.out_b, residual=x, drop_p=p_tr,
+                           seed=sd(_site("enc", i, 1)))
             x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "enc%d.ln1" % i)
             h, hq = self._lin(f8, x1, x1q, "enc%d.l1" % i, L.l1_w, L.l1_b, q_site="enc%d.h" % i,
                               relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
@@ -352,22 +365,26 @@ class Engine:
             qkv = self._lin(f8, y, yq, "dec%d.sa" % i, L.sa_w, L.sa_b)
             o = torch.empty(B * T, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, T, device=dev)
+            q8, oq = self._attn_q8(f8, o, "dec%d.o" % i)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
                          D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)),
-                         drop_mask=amask(("dec", i), T, T))
-            y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr, seed=sd(_site("dec", i, 1)))
+                         drop_mask=amask(("dec", i), T, T), q8=q8)
+            y1 = self._lin(f8, o, oq, "dec%d.sao" % i, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr,
+                           seed=sd(_site("dec", i, 1)))
             x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "dec%d.ln1" % i)
             qc = self._lin(f8, x1, x1q, "dec%d.cq" % i, L.cq_w, L.cq_b)
             kvc = kvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             oc = torch.empty(B * T, d, dtype=dt, device=dev)
             lsec = torch.empty(B, H, T, device=dev)
+            q8, ocq = self._attn_q8(f8, oc, "dec%d.oc" % i)
             ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                          causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)),
-                         drop_mask=amask(("cross", i), T, S))
+                         drop_mask=amask(("cross", i), T, S), q8=q8)
             if need_weights:
                 ops.attn_weights(qc, kvc[:, :d], lsec, wts[i], B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                                  scale=scale)
-            y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1, drop_p=p_tr, seed=sd(_site("dec", i, 3)))
+            y2 = self._lin(f8, oc, ocq, "dec%d.cao" % i, L.ca_ow, L.ca_ob, residual=x1, drop_p=p_tr,
+                           seed=sd(_site("dec", i, 3)))
             x2, m2, r2, x2q = self._ln_q(f8, y2, L.n2, dt, "dec%d.ln2" % i)
             h, hq = self._lin(f8, x2, x2q, "dec%d.l1" % i, L.l1_w, L.l1_b, q_site="dec%d.h" % i,
                               relu=True, drop_p=p_tr, seed=sd(_site("dec", i, 4)))

@@ -6,9 +6,10 @@ LayerNorm run on the block-scaled fp8 MFMA (`smer_gemm_fp8`): the QKV
 in-projections of layers >= 1, FFN1, the decoder's cross-attention Q and the
 stacked cross-attention K/V of the memory (`transformer.py:389,393,459,463,
 467`); FFN2 too when FFN1 writes an e4m3 copy of its output
-(engine.FP8_FFN2, off by default: measured slower at C4).  Out-projections
-(input: attention output) and the vocab head stay bf16; master weights fp32,
-working weights bf16.
+(engine.FP8_FFN2, off by default: measured slower at C4), and the attention
+out-projections, whose input the attention forward writes in e4m3 beside O
+(FP8_ATTN_OUT).  The vocab head stays bf16; master weights fp32, working
+weights bf16.
 
 Backward (FP8_DGRAD): the dgrad products whose input gradient comes from a
 LayerNorm backward, the FFN2 dgrad or the attention backward run as
@@ -50,6 +51,9 @@ FP8_DGRAD = os.environ.get("SMER_FP8_DGRAD", "1") != "0"
 # ... including the QKV / cross-Q dgrads fed by the attention backward
 # (SMER_FP8_ATTN_DGRAD=0: those stay bf16, A/B)
 FP8_ATTN_DGRAD = os.environ.get("SMER_FP8_ATTN_DGRAD", "1") != "0"
+# fp8 attention out-projections in the forward: the attention kernel writes
+# the e4m3 copy of its output (SMER_FP8_ATTN_OUT=0: bf16, A/B)
+FP8_ATTN_OUT = os.environ.get("SMER_FP8_ATTN_OUT", "1") != "0"
 
 
 class Fp8Forward:
@@ -105,9 +109,13 @@ class Fp8Forward:
         out = []
         for i, L in enumerate(W.enc):
             out += [("enc%d.in" % i, L.in_w), ("enc%d.l1" % i, L.l1_w), ("enc%d.l2" % i, L.l2_w)]
+            if FP8_ATTN_OUT:
+                out.append(("enc%d.out" % i, L.out_w))
         for i, L in enumerate(W.dec):
             out += [("dec%d.sa" % i, L.sa_w), ("dec%d.cq" % i, L.cq_w), ("dec%d.l1" % i, L.l1_w),
                     ("dec%d.l2" % i, L.l2_w)]
+            if FP8_ATTN_OUT:
+                out += [("dec%d.sao" % i, L.sa_ow), ("dec%d.cao" % i, L.ca_ow)]
         if getattr(W, "ckv_all", None) is not None:
             out.append(("ckv", W.ckv_all))
         return out

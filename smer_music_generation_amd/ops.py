@@ -211,10 +211,20 @@ def _check_attn_p(p):
 
 
 def attn_fwd(q, k, v, o, lse, *, B, H, Lq, Lk, D, kpm=None, causal=False, scale, drop_p=0.0,
-             seed=0, drop_mask=None, drop_mask_in=False):
+             seed=0, drop_mask=None, drop_mask_in=False, q8=None):
     """drop_mask: keep-bit buffer the forward fills (hashing) for the
-    backward, or, with drop_mask_in, reads (from attn_drop_mask_gen)."""
+    backward, or, with drop_mask_in, reads (from attn_drop_mask_gen).
+    q8 (bf16): (o8, qs, amax) -- the e4m3 copy e4m3(o * qs[0]) of the output,
+    max|o| folded into amax (smer_attn_fwd_fp8)."""
     _check_attn_p(drop_p)
+    if q8 is not None:
+        if dtype_code(q.dtype) != BF16:
+            raise RuntimeError("attn_fwd: the e4m3 copy needs bf16")
+        o8, qs, amax = q8
+        call("smer_attn_fwd_fp8", B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v), _p(o),
+             _ld(o), _p(lse), _p(kpm), int(causal), float(scale), float(drop_p), int(seed) & 0xFFFFFFFF,
+             _p(drop_mask), int(bool(drop_mask_in)), _p(o8), _ld(o8), _p(qs), _p(amax), _stream())
+        return
     call("smer_attn_fwd", dtype_code(q.dtype), B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k),
          _p(v), _ld(v), _p(o), _ld(o), _p(lse), _p(kpm), int(causal), float(scale),
          float(drop_p), int(seed) & 0xFFFFFFFF, _p(drop_mask), int(bool(drop_mask_in)), _stream())

@@ -390,6 +390,29 @@ def test_attention_first_keys_far_below(causal):
         assert torch.isfinite(t.float()).all()
 
 
+@pytest.mark.parametrize("qg2", [False, True])
+def test_attention_fwd_e4m3_copy(qg2):
+    """smer_attn_fwd_fp8: O and lse are the plain forward's bit for bit, the
+    copy is e4m3(o * qs) (nearest-even, saturated), amax = max|o|."""
+    O = ops()
+    B, H, L, D = (16, 8, 512, 64) if qg2 else (2, 3, 200, 64)
+    q, k, v, kpm = _attn_inputs(B, H, L, L, D, torch.bfloat16, True)
+    o0 = torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16)
+    lse0 = torch.empty(B, H, L, device=dev)
+    O.attn_fwd(q, k, v, o0, lse0, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, scale=0.125, drop_p=0.1, seed=9)
+    o, lse = torch.empty_like(o0), torch.empty_like(lse0)
+    o8 = torch.zeros(B * L, H * D, device=dev, dtype=torch.uint8)
+    qs = torch.tensor([150.0], device=dev)
+    amax = torch.zeros(1, dtype=torch.int32, device=dev)
+    O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, scale=0.125, drop_p=0.1, seed=9,
+               q8=(o8, qs, amax))
+    torch.cuda.synchronize()
+    assert torch.equal(o, o0) and torch.equal(lse, lse0)
+    want = (o.float() * 150.0).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(o8, want)
+    assert amax.view(torch.float32).item() == o.float().abs().max().item()
+
+
 @pytest.mark.parametrize("kg2", [False, True])
 def test_attention_bwd_e4m3_copies(kg2):
     """smer_attn_bwd_fp8: the bf16 gradients are the plain backward's bit for
