@@ -96,6 +96,13 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 __device__ __forceinline__ bf16x8 words_bf16x8(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return __builtin_bit_cast(bf16x8, u32x4{a, b, c, d});
 }
+// the lane index as an opaque value (v_mbcnt): hipcc cannot fold it into a
+// thread-index register it would keep live across a loop
+__device__ __forceinline__ int lane_id_fresh() {
+  int r;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(r));
+  return r;
+}
 // each 16-bit half -> 0xFFFF if its top bit is set, else 0 (v_pk_ashrrev_i16)
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t half_masks(uint32_t x) {
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
-      if (kp) npad = kp[min((t + 1) * KVB + lane, Lk - 1)];  // every lane: no exec-masked join
+      if (kp) npad = kp[min((t + 1) * KVB + (Q8 ? lane_id_fresh() : lane), Lk - 1)];  // every lane: no exec-masked join
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
@@ -405,10 +412,13 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
       asm volatile("" : "+v"(npad));  // keeps the compare (and its wait) here
       if (tid < KVB) {  // wave 0
-        const bool pk = (t + 1) * KVB + tid >= Lk || npad;
-        kbias[cur ^ 1][tid] = pk ? -INFINITY : 0.f;
+        // Q8: the lane index from v_mbcnt (wave 0: lane == tid), not a
+        // register kept across the loop (the e4m3-copy instance spilled it)
+        const int kl = Q8 ? lane_id_fresh() : tid;
+        const bool pk = (t + 1) * KVB + kl >= Lk || npad;
+        kbias[cur ^ 1][kl] = pk ? -INFINITY : 0.f;
         const uint64_t any = __ballot(pk);
-        if (tid == 0) kpad[cur ^ 1] = any != 0ull;
+        if (kl == 0) kpad[cur ^ 1] = any != 0ull;
       }
     }
     __syncthreads();
@@ -416,9 +426,15 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
   constexpr bool w8 = Q8;
   const float q8s = w8 ? *q8.qs : 1.f;
   float am = 0.f;
+  // Q8: lane indices re-formed here, so hipcc does not share the row
+  // products with the prologue's and keep them live across the key loop
+  // (the copy's extra row address then spilled, with a reload per tile)
+  int le = lane;
+  if constexpr (Q8) asm volatile("" : "+v"(le));
+  const int ge = le >> 4, ce = le & 15;
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
-    const int qi = q0w + gq * 16 + c16;
+    const int qi = q0w + gq * 16 + ce;
     float l = l_run[gq] + __shfl_xor(l_run[gq], 16, 64);
     l += __shfl_xor(l, 32, 64);
     if (qi >= Lq) continue;
@@ -429,17 +445,17 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       bf16x4 w;
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(acc[gq][dt][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = w;
+      *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * ge) = w;
       if constexpr (Q8) {  // e4m3 copy of the stored (bf16-rounded) values
         float f[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) f[r] = (float)w[r];
-        *reinterpret_cast<uint32_t*>(q8.dq + (long)(b * Lq + qi) * q8.lddq + h * D + dt * 16 + 4 * g) =
+        *reinterpret_cast<uint32_t*>(q8.dq + (long)(b * Lq + qi) * q8.lddq + h * D + dt * 16 + 4 * ge) =
             smer_q8x4(f, q8s);
         am = fmaxf(am, smer_absmax4(f));
       }
     }
-    if (g == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_ref[gq] + log2f(l)) * LN2_F : INFINITY;
+    if (ge == 0) lse[(long)bh * Lq + qi] = l > 0.f ? (m_ref[gq] + log2f(l)) * LN2_F : INFINITY;
   }
   if constexpr (Q8) smer_amax_commit(q8.amax, am);
 }
