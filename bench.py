@@ -453,6 +453,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-roofline", dest="roofline", action="store_false")
     ap.add_argument("--grad-wire", dest="grad_wire", choices=("fp32", "bf16"), default="fp32",
                     help="DP gradient all-reduce dtype of the headline step (fp32 = parity)")
+    ap.add_argument("--global-batch", dest="global_batch", type=int, default=0,
+                    help="strong scaling: fix the GLOBAL batch at this many sequences, split "
+                         "evenly over the ranks (default 0: weak scaling, --batch per rank). "
+                         "Under DP without it, a 'train_strong' block still reports the step at "
+                         "global batch --batch split over the ranks (SURVEY §8e: report both)")
     ap.add_argument("--dry-run", dest="dry_run", action="store_true",
                     help="launcher / DP plumbing check on CPU over gloo (no GPU, no HIP): "
                          "rank-0 broadcast + the bucketed gradient all-reduce, C1 model")
@@ -481,6 +486,22 @@ def launch_ranks(n, argv):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+def per_rank_batch(global_batch, world):
+    """Strong scaling: the global batch split evenly over the ranks."""
+    if global_batch % world:
+        raise SystemExit("--global-batch %d is not divisible by %d ranks" % (global_batch, world))
+    return global_batch // world
+
+
+def scaling_modes(args, world):
+    """Both DP scalings of the C2 step: weak = --batch per rank,
+    strong = the global batch (--global-batch, else --batch) split over the
+    ranks."""
+    g = args.global_batch or args.batch
+    return {"weak": {"per_rank_batch": args.batch, "global_batch": args.batch * world},
+            "strong": {"per_rank_batch": per_rank_batch(g, world), "global_batch": g}}
 
 
 def dry_run(args, rank, world):
@@ -515,7 +536,10 @@ def dry_run(args, rank, world):
     want = world * (world + 1) / 2
     return {"seconds": dt, "params_in_sync_at_init": in_sync,
             "allreduce_ok": bool(torch.all(g == want).item()),
-            "bytes_per_step": grad.numel() * (2 if args.grad_wire == "bf16" else 4)}
+            "bytes_per_step": grad.numel() * (2 if args.grad_wire == "bf16" else 4),
+            # the gradient exchange is the same in both modes (one flat buffer
+            # of parameters); what changes is the per-rank batch
+            "scaling_modes": scaling_modes(args, world)}
 
 
 def data_feed(per_gpu_tokens_per_s, seconds=3.0):
@@ -560,7 +584,8 @@ def main():
                 "config": {"workload": "C1 model, rank-0 broadcast + bucketed gradient "
                                        "all-reduce (gloo)", "parallelism": "dp%d" % world},
                 "params_in_sync_at_init": r["params_in_sync_at_init"],
-                "allreduce_ok": r["allreduce_ok"], "bytes_per_step": r["bytes_per_step"]}))
+                "allreduce_ok": r["allreduce_ok"], "bytes_per_step": r["bytes_per_step"],
+                "scaling_modes": r["scaling_modes"]}))
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
@@ -574,13 +599,29 @@ def main():
     _lib.load()
 
     wire = torch.bfloat16 if args.grad_wire == "bf16" else None
-    tr = bench_train(args, dev, rank, world, grad_wire=wire)
+    strong = args.global_batch > 0
+    if strong:  # the headline itself at a fixed global batch
+        import copy
+        head = copy.copy(args)
+        head.batch = per_rank_batch(args.global_batch, world)
+    else:
+        head = args
+    tr = bench_train(head, dev, rank, world, grad_wire=wire)
+    # DP, weak headline: the strong-scaling step beside it (global batch
+    # --batch split over the ranks), SURVEY §8e "report both"
+    tr_strong = None
+    if world > 1 and not strong:
+        import copy
+        a = copy.copy(args)
+        a.roofline = False
+        a.batch = per_rank_batch(args.batch, world)
+        tr_strong = bench_train(a, dev, rank, world, grad_wire=wire)
     # DP only: the same step with the opt-in bf16 gradient all-reduce
     # (half the xGMI bytes), reported beside the fp32 (parity) headline
     tr_alt = None
     if world > 1 and wire is None:
         import copy
-        a = copy.copy(args)
+        a = copy.copy(head)
         a.roofline = False
         tr_alt = bench_train(a, dev, rank, world, grad_wire=torch.bfloat16)
     c4 = bench_train_c4(args, dev, rank, world, "fp8") if args.c4 else None
@@ -625,16 +666,23 @@ def main():
             "value": round(tr["tokens_per_s"], 1), "unit": "train tokens/s (B*(S+T))",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tr["ms_per_step"], 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic SMER-grammar token batches (seeded), random xavier_normal weights",
             "config": {"workload": "C2 train step: 6+6 layers d512 h8 ff2048 V309, per-GPU "
                                    "B=%d S=%d T=%d, dropout %.1f, fused WCE + Adam%s"
-                                   % (args.batch, args.seq, args.tgt, args.dropout,
+                                   % (head.batch, args.seq, args.tgt, args.dropout,
                                       " + RCCL grad all-reduce" if world > 1 else ""),
-                       "global_batch": args.batch * world, "seq_len": args.seq,
+                       "global_batch": head.batch * world, "seq_len": args.seq,
                        "tgt_len": args.tgt, "parallelism": "dp%d" % world},
             "train": {k: (round(val, 4) if isinstance(val, float) else val)
                       for k, val in tr.items() if k != "gemm"},
+            "train_strong": tr_strong and {
+                "scaling": "strong", "global_batch": args.batch,
+                "per_rank_batch": args.batch // world,
+                "tokens_per_s": round(tr_strong["tokens_per_s"], 1),
+                "ms_per_step": round(tr_strong["ms_per_step"], 3),
+                "note": "same step at a fixed global batch split over the ranks (the headline "
+                        "is weak scaling: B per rank)"},
             "train_bf16_allreduce": tr_alt and {
                 "tokens_per_s": round(tr_alt["tokens_per_s"], 1),
                 "ms_per_step": round(tr_alt["ms_per_step"], 3),
@@ -657,8 +705,11 @@ def main():
                                                      "KV-cached), tokens/s")},
             "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
                                           "S=2048 T=512",
-                                "dtype": "fp8 (e4m3 QKV/FFN/cross forward GEMMs, delayed "
-                                         "scaling; bf16 elsewhere)",
+                                "dtype": "fp8 (e4m3 forward GEMMs: QKV, attention out-"
+                                         "projections, FFN1, cross-attention Q and K/V; e4m3 "
+                                         "dgrads: FFN2, FFN1, out-projections, QKV, cross Q, "
+                                         "memory; delayed per-tensor scaling; weight gradients, "
+                                         "attention, FFN2 forward and the vocab head bf16)",
                                 "value": round(c4["tokens_per_s"], 1),
                                 "ms_per_step": round(c4["ms_per_step"], 2),
                                 "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),

@@ -244,18 +244,21 @@ class Engine:
         si = f8.site(site)
         q = torch.empty(M, N, dtype=torch.uint8, device=x.device)
         ops.layernorm_fp8(x, wb[0], wb[1], y, mean, rstd, q, f8.qs_of(si), f8.amax_of(si))
-        return y, mean, rstd, (q, si)
+        # no amax history yet: the copy only records this forward's range
+        return y, mean, rstd, ((q, si) if f8.record_fwd(si) else None)
 
     @staticmethod
-    def _attn_q8(f8, o, site):
-        """fp8 forward: (q8 argument of ops.attn_fwd, (e4m3 copy of o, site))
-        so that the out-projection reads the attention output in e4m3."""
+    def _attn_q8(f8, o, site, D):
+        """fp8 forward: (q8 argument of ops.attn_fwd, (e4m3 copy of o, site)
+        or None) so that the out-projection reads the attention output in
+        e4m3.  The copy instance is built for head dim 64 only; other head
+        dims keep bf16 out-projections."""
         from .fp8 import FP8_ATTN_OUT
-        if f8 is None or not FP8_ATTN_OUT:
+        if f8 is None or not FP8_ATTN_OUT or D != 64:
             return None, None
         si = f8.site(site)
         q = torch.empty(o.shape, dtype=torch.uint8, device=o.device)
-        return (q, f8.qs_of(si), f8.amax_of(si)), (q, si)
+        return (q, f8.qs_of(si), f8.amax_of(si)), ((q, si) if f8.record_fwd(si) else None)
 
     def _lin(self, f8, x, xq, wname, w, b, q_site=None, **epi):
         """x @ w^T + epilogue: on the fp8 MFMA when x has an e4m3 copy xq and
@@ -267,8 +270,8 @@ class Engine:
         if q_site is not None and not FP8_FFN2:
             return self._lin(f8, x, xq, wname, w, b, **epi), None
         if f8 is not None and xq is not None:
-            from .fp8 import eligible
-            if eligible(M, N, K) and epi.get("gate") is None:
+            from .fp8 import FWD_GROUPS, eligible, fwd_group
+            if eligible(M, N, K) and epi.get("gate") is None and fwd_group(wname) in FWD_GROUPS:
                 w8, winv = f8.weight(wname, w)
                 out = torch.empty(M, N, dtype=x.dtype, device=x.device)
                 if q_site is not None:
@@ -276,7 +279,7 @@ class Engine:
                     q = torch.empty(M, N, dtype=torch.uint8, device=x.device)
                     ops.gemm_fp8_q(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, q8=q,
                                    qs=f8.qs_of(si), amax=f8.amax_of(si), **epi)
-                    return out, (q, si)
+                    return out, ((q, si) if f8.record_fwd(si) else None)
                 ops.gemm_fp8(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, **epi)
                 return out
         out = ops.linear(x, w, b, **epi)
@@ -335,7 +338,7 @@ class Engine:
             qkv = self._lin(f8, x, xq, "enc%d.in" % i, L.in_w, L.in_b)
             o = torch.empty(B * S, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, S, device=dev)
-            q8, oq = self._attn_q8(f8, o, "enc%d.o" % i)
+            q8, oq = self._attn_q8(f8, o, "enc%d.o" % i, D)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
                          D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)),
                          drop_mask=amask(("enc", i), S, S), q8=q8)
@@ -365,7 +368,7 @@ class Engine:
             qkv = self._lin(f8, y, yq, "dec%d.sa" % i, L.sa_w, L.sa_b)
             o = torch.empty(B * T, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, T, device=dev)
-            q8, oq = self._attn_q8(f8, o, "dec%d.o" % i)
+            q8, oq = self._attn_q8(f8, o, "dec%d.o" % i, D)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
                          D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)),
                          drop_mask=amask(("dec", i), T, T), q8=q8)
@@ -376,7 +379,7 @@ class Engine:
             kvc = kvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             oc = torch.empty(B * T, d, dtype=dt, device=dev)
             lsec = torch.empty(B, H, T, device=dev)
-            q8, ocq = self._attn_q8(f8, oc, "dec%d.oc" % i)
+            q8, ocq = self._attn_q8(f8, oc, "dec%d.oc" % i, D)
             ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                          causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)),
                          drop_mask=amask(("cross", i), T, S), q8=q8)
@@ -436,6 +439,22 @@ class Engine:
         if side is not None:
             torch.cuda.current_stream(side[0].device).wait_stream(side[0])
 
+    @staticmethod
+    def _hook(side, hook, name):
+        """A layer's gradients are final: call hook(name) (GradBucketer issues
+        that range's all-reduce).  With the weight-gradient stream, every
+        gradient write of a layer range is queued on it (weight / bias
+        gradients and the LayerNorm parameter reductions), so the hook runs
+        with that stream current: the collective waits for the side stream
+        only and the main stream's dgrad chain never joins it mid-backward
+        (the overlap survives under DP).  The main stream joins once, at the
+        end of backward."""
+        if side is None:
+            hook(name)
+            return
+        with torch.cuda.stream(side[0]):
+            hook(name)
+
     def backward(self, ctx, dlog_pad, hook=None):
         """dlog_pad: [B*T, Vp] activation dtype (cols >= V zero).  Accumulates
         every parameter gradient into the flat grad buffer.  `hook(name)` is
@@ -493,14 +512,16 @@ class Engine:
                 if wt is not None and eligible(M, w.shape[1], w.shape[0]):
                     out = torch.empty(M, w.shape[1], dtype=dt, device=dev)
                     if q_site is None:
-                        ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, **epi)
-                        return out, None
-                    si = f8.site(q_site)
-                    q = torch.empty(M, w.shape[1], dtype=torch.uint8, device=dev)
-                    ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, q8=q, qs=f8.qs_of(si),
-                                    amax=f8.amax_of(si), **epi)
-                    f8.record_bwd(q_site)
-                    return out, ((q, si) if q_site in f8.bwd_ready else None)
+                        if ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, **epi):
+                            return out, None
+                    else:
+                        si = f8.site(q_site)
+                        q = torch.empty(M, w.shape[1], dtype=torch.uint8, device=dev)
+                        if ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, q8=q,
+                                           qs=f8.qs_of(si), amax=f8.amax_of(si), **epi):
+                            f8.record_bwd(q_site)
+                            return out, ((q, si) if q_site in f8.bwd_ready else None)
+            # bf16 (also whenever the fp8 kernel declined the shape: nothing launched)
             return ops.linear_dgrad(g, w, **epi), None
 
         # vocab head
@@ -515,8 +536,7 @@ class Engine:
         ops.layernorm_bwd(g_out, y_last, mo, ro, W.dec_norm[0], dy, dgamma=G.dec_norm[0],
                           dbeta=G.dec_norm[1], param_stream=ps)
         if hook:
-            self._join(side)
-            hook("head")
+            self._hook(side, hook, "head")
         # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
         # one dgrad GEMM (K = L*2d) after the decoder loop gives dmemory
         dkvc_all = torch.empty(Ms, self.n_dec * 2 * d, dtype=dt, device=dev)
@@ -576,12 +596,13 @@ class Engine:
             wg(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             dy, _ = dgrad(dqkvq, dqkv, "dec%d.sa" % i, L.sa_w, residual=dy1)
             if hook:
-                self._join(side)
-                hook("dec%d" % i)
+                self._hook(side, hook, "dec%d" % i)
         d_tgt = dy
         if self.n_dec:
             if (cross8 is not None and "b.cross" in f8.bwd_ready and f8.weight_t("ckv") is not None
                     and eligible(Ms, d, self.n_dec * 2 * d)):
+                # bf16 output (the bf16 path sums into fp32): its rounding,
+                # unit roundoff 2^-9, is far below the e4m3 operands' 2^-4
                 dmem, _ = dgrad((cross8[1], cross8[0]), dkvc_all, "ckv", W.ckv_all)
             else:
                 dmem = ops.linear_dgrad(dkvc_all, W.ckv_all, out_f32=torch.empty(Ms, d, device=dev))
@@ -617,8 +638,7 @@ class Engine:
             wg(dqkv, x_in, GL.in_w, db=GL.in_b)
             dx, _ = dgrad(dqkvq, dqkv, "enc%d.in" % i, L.in_w, residual=dy1)
             if hook:
-                self._join(side)
-                hook("enc%d" % i)
+                self._hook(side, hook, "enc%d" % i)
         # shared embedding (model.py:76): both streams scatter into one table
         ops.embed_bwd(G.emb, math.sqrt(d), [(ctx.src_ids, dx, ctx.p_pos, sd(_SITE["pe_src"])),
                                             (ctx.tgt_ids, d_tgt, ctx.p_pos, sd(_SITE["pe_tgt"]))])

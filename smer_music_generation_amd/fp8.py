@@ -30,8 +30,9 @@ Scaling (no standalone quantise pass over activations):
     q = e4m3(y * qs) beside its bf16 output and folds max|y| into an amax
     slot of this forward (atomicMax on float bits);
   * qs for forward t comes from the amax recorded in forward t-1
-    (`smer_fp8_scales`: qs = 448 / amax, inv = amax / 448; 1 / 1 for the
-    first forward, which suits LayerNorm / ReLU outputs of O(1));
+    (`smer_fp8_scales`: qs = 448 / amax, inv = amax / 448); a site with no
+    recorded amax yet (the first forward) still writes its copy and amax but
+    its consumer GEMM runs bf16 (`record_fwd`), as the backward sites do;
   * weights are quantised once per optimizer step (current scaling: amax of
     the new weights, then the cast), all of them in one batched call
     (`smer_fp8_quantize_segments`: a memset + 2 launches per step), into
@@ -55,6 +56,25 @@ FP8_ATTN_DGRAD = os.environ.get("SMER_FP8_ATTN_DGRAD", "1") != "0"
 # the e4m3 copy of its output (SMER_FP8_ATTN_OUT=0: bf16, A/B)
 FP8_ATTN_OUT = os.environ.get("SMER_FP8_ATTN_OUT", "1") != "0"
 
+# forward contraction groups that run on the fp8 MFMA (tests / tools switch
+# groups off to measure each one's numerical effect): "qkv" self-attention
+# in-projections, "cross" the cross-attention Q and stacked K/V projections,
+# "ffn" FFN1 (and FFN2 with engine.FP8_FFN2), "out" the attention
+# out-projections (with FP8_ATTN_OUT)
+FWD_GROUPS = set(g for g in os.environ.get("SMER_FP8_FWD", "qkv,cross,ffn,out").split(",") if g)
+
+
+def fwd_group(wname):
+    """Forward group of an fp8 weight name (see gemm_weights)."""
+    tail = wname.split(".")[-1]
+    if tail in ("in", "sa"):
+        return "qkv"
+    if tail in ("cq", "ckv") or wname == "ckv":
+        return "cross"
+    if tail in ("l1", "l2"):
+        return "ffn"
+    return "out"
+
 
 class Fp8Forward:
     def __init__(self, engine, device):
@@ -77,6 +97,8 @@ class Fp8Forward:
         self._segt = None
         self._bwd_recorded = set()  # backward sites whose amax this step records
         self.bwd_ready = set()      # ... recorded in an earlier step: scales valid
+        self._fwd_recorded = set()  # forward site indices whose amax this forward records
+        self.fwd_ready = set()      # ... recorded by an earlier calibrating forward
 
     def begin(self, W=None, training=True):
         """Start a forward: this forward's scales from the previous one's
@@ -94,6 +116,8 @@ class Fp8Forward:
         if calibrate:
             self.bwd_ready |= self._bwd_recorded
             self._bwd_recorded = set()
+            self.fwd_ready |= self._fwd_recorded
+            self._fwd_recorded = set()
             prev, nxt = self.amax[self.t % 2], self.amax[(self.t + 1) % 2]
             ops.fp8_scales(prev, self.qs, self.inv, nxt)
             self.cur = nxt
@@ -165,6 +189,17 @@ class Fp8Forward:
     def record_bwd(self, name):
         """A backward producer wrote site `name`'s amax this step."""
         self._bwd_recorded.add(name)
+
+    def record_fwd(self, i):
+        """A forward producer wrote site i's amax into this forward's slot.
+        Returns whether site i's scale is delayed-scaling valid now, i.e. an
+        earlier calibrating forward recorded its amax.  A site without that
+        history (the first training forward, a new site) feeds a bf16 GEMM
+        instead of its e4m3 copy: no forward contraction ever runs on the
+        unit scale (qs = 1) of a site whose range was never measured."""
+        if self.cur is not self._eval_amax:
+            self._fwd_recorded.add(i)
+        return i in self.fwd_ready
 
     def _quantize_weights(self, W):
         ws = [(n, w) for n, w in self.gemm_weights(W) if w.is_contiguous() and w.numel() % 8 == 0]

@@ -76,11 +76,21 @@ def test_bf16_wgrad_stream_bitexact_and_ranges_final_at_hook(monkeypatch):
     ranges = layer_ranges(m)
     seen = {}
 
+    streams = set()
+
     def hook(name):
+        # runs with the stream the engine issues the range's all-reduce from
+        # (the weight-gradient stream): a copy queued there sees the range final
         a, b = ranges[name]
-        seen[name] = m.flat_grad()[a:b].clone()   # on the main stream, at hook time
+        streams.add(torch.cuda.current_stream().cuda_stream)
+        seen[name] = m.flat_grad()[a:b].clone()
+    main = torch.cuda.current_stream().cuda_stream
     g1 = _fwd_bwd(m, bt, hook)
     assert torch.equal(g0, g1)
+    # the layer hooks ran off the main stream (the main stream never joined
+    # the weight-gradient stream mid-backward); "embedding" comes after the
+    # final join, on the main stream
+    assert len(streams - {main}) == 1, streams
     assert set(seen) == set(ranges)
     for name, snap in seen.items():
         a, b = ranges[name]
@@ -160,25 +170,40 @@ def _free_port():
 
 
 @pytest.mark.timeout(300)
-def test_two_ranks_gloo_engine_matches_single_process(tmp_path):
-    from smer_music_generation_amd.train import Trainer
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_two_ranks_gloo_engine_matches_single_process(tmp_path, precision):
+    """bf16: the weight gradients run on the side stream and every layer
+    hook issues its all-reduce from there (no main-stream join); the ranks'
+    summed gradients still equal the single process's, range by range, to
+    bf16 rounding (different per-rank M picks other tilings)."""
+    from smer_music_generation_amd.train import Trainer, layer_ranges
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path)]
+           os.path.join(ROOT, "tests", "dp_engine_worker.py"), str(tmp_path), precision]
     env = dict(os.environ)
     env["OMP_NUM_THREADS"] = "2"
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    m, v = build("cuda")
+    m, v = build("cuda", precision)
     b = make_batch(v)
     bt = {k: torch.from_numpy(np.asarray(x)).to("cuda") for k, x in b.items()}
     loss = Trainer(m, v).step(bt)
     g = m.flat_grad().cpu()
+    ranges = layer_ranges(m)
     for rk in range(2):
         got = torch.load(os.path.join(tmp_path, "rank%d.pt" % rk), weights_only=True)
-        assert abs(float(got["loss"]) - loss.item()) < 1e-5 * max(1.0, loss.item())
-        err = float((got["grad"] - g).norm() / g.norm())
-        # fp32 summation order differs: a rank's decoder Linears have M = 64
-        # rows and run the skinny fp32 kernel (K split over 4 waves), the
-        # single process's M = 128 the tile kernel; measured 1.0e-5
-        assert err < 5e-5, (rk, err)
+        if precision == "fp32":
+            assert abs(float(got["loss"]) - loss.item()) < 1e-5 * max(1.0, loss.item())
+            err = float((got["grad"] - g).norm() / g.norm())
+            # fp32 summation order differs: a rank's decoder Linears have M = 64
+            # rows and run the skinny fp32 kernel (K split over 4 waves), the
+            # single process's M = 128 the tile kernel; measured 1.0e-5
+            assert err < 5e-5, (rk, err)
+        else:
+            assert abs(float(got["loss"]) - loss.item()) < 2e-2 * max(1.0, loss.item())
+            for name, (a, b_) in ranges.items():
+                ref = g[a:b_]
+                err = float((got["grad"][a:b_] - ref).norm() / max(ref.norm().item(), 1e-12))
+                # a hook that raced its side-stream gradients would leave a
+                # range O(1) wrong; bf16 rounding moves it by a few 1e-3
+                assert err < 5e-2, (rk, name, err)

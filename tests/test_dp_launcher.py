@@ -37,6 +37,17 @@ def test_bench_gpus2_launches_two_ranks(wire):
     assert line["params_in_sync_at_init"] is True
     assert line["allreduce_ok"] is True
     assert line["dry_run"] is True and line["value"] is None
+    # both DP scalings -- weak (B per rank) and strong (the
+    # global batch split over the ranks)
+    modes = line["scaling_modes"]
+    assert modes["weak"] == {"per_rank_batch": 32, "global_batch": 64}
+    assert modes["strong"] == {"per_rank_batch": 16, "global_batch": 32}
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_strong_scaling_split():
+    line = _bench_line("--global-batch", "48")
+    assert line["scaling_modes"]["strong"] == {"per_rank_batch": 24, "global_batch": 48}
 
 
 def _init_worker(rank, world, port, out_dir, broadcast):

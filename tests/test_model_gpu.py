@@ -131,9 +131,12 @@ def _oracle_batch(v, B, S, T, seed):
     return b
 
 
-@pytest.mark.parametrize("d,H,F,B,S,T", [(128, 4, 256, 4, 128, 32), (256, 4, 512, 2, 192, 64)])
+@pytest.mark.parametrize("d,H,F,B,S,T", [(128, 4, 2048, 4, 128, 32), (128, 4, 256, 4, 128, 32),
+                                          (256, 4, 512, 2, 192, 64)])
 def test_train_step_matches_oracle_larger(d, H, F, B, S, T):
-    """fp32 engine vs the oracle at C1-like shapes (head dim 32 / 64)."""
+    """fp32 engine vs the oracle: BASELINE configs[0] / C1 exactly (2+2
+    layers d128 h4, F = 2048 as train.py:258 fixes it, B4 S128 T32), and
+    C1-like shapes with smaller F (head dim 32 / 64)."""
     from oracle import ref_cpu
     from smer_music_generation_amd.model import ScoreTransformer
     from smer_music_generation_amd.train import Trainer
