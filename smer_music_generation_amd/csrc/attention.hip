@@ -569,7 +569,14 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   __syncthreads();
   smer_vm_drain();  // prologue loads retired before the loop (common.h)
   // K pre-scaled by c = scale * log2(e) and the S chain seeded with -lse
-  // (log2 units): p = 2^acc leaves the MFMA with no per-score arithmetic
+  // (log2 units): p = 2^acc leaves the MFMA with no per-score arithmetic.
+  // K is this kernel's register-resident operand, so the bf16 rounding of
+  // the product lands on K here and on Q in the forward / dQ kernels: the
+  // recomputed scores differ from the forward's by |s| * 2^-9 at most (one
+  // bf16 rounding each, the size of the bf16 rounding of Q and K
+  // themselves), so P matches the forward's lse to ~|s| * 2^-8 relative.
+  // Held by the dK / dV checks against fp32 torch in tests/test_kernels_gpu.py
+  // (bf16 tolerance), DESIGN.md §8.
 #pragma unroll
   for (int gk = 0; gk < KG; ++gk)
 #pragma unroll

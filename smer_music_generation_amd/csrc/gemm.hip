@@ -46,6 +46,8 @@ struct GemmEpi {
   long ldq8;
   const float* q8_scale;
   unsigned* q8_amax;
+  // diagnostics (smer_gemm_debug_stamps): per-wave s_memtime phase stamps
+  unsigned long long* dbg;
 };
 
 template <typename T>
@@ -850,6 +852,471 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
 }
 
 // ---------------------------------------------------------------------------
+// Staggered 256x256 bf16 GEMM (round 4) for the forward (NT) and dgrad (NN)
+// shapes with whole 256 tiles and a bf16 output (the streamed-epilogue
+// cases).  Same tile and wave layout as gemm256_bf16_kernel (8 waves, 2 along
+// M x 4 along N, 128x64 outputs per wave), a different schedule:
+//
+//  * LDS holds four 32-deep k-step slots (A [256][32] + B, 32 KiB each),
+//    filled by LDS-DMA three k-steps ahead, so two slots are always in
+//    flight across the barriers (counted vmcnt, never 0 in the loop);
+//  * the two M halves of the workgroup run one barrier apart (waves 4-7 pass
+//    one extra barrier at the start, waves 0-3 one at the end): on every
+//    SIMD one wave issues its 12 fragment reads while its partner runs its
+//    32 MFMAs, then they swap -- the LDS latency of a k-step hides under the
+//    partner's matrix work instead of stalling both waves together;
+//  * roles: waves 4-7 issue every LDS-DMA (operands and the epilogue's
+//    residual / gate rows) and never store, waves 0-3 issue every global
+//    store of the epilogue and never load.  gfx9's vmcnt retires in issue
+//    order and counts stores too, so a wave that stores and then waits for
+//    its next operand DMA waits for its stores to drain to HBM: at K = 512
+//    (FFN1: 134 MB of output) that drain was 26 of the old kernel's 90 us.
+//    Here the loaders' counters hold only loads and the storers never wait,
+//    so a tile's output drains under the next tile's k-loop.
+//  * every LDS-DMA is an asm statement (M0 set inside it), invisible to
+//    hipcc's wait bookkeeping, which otherwise makes compiler-visible LDS
+//    accesses wait vmcnt(0) for any DMA it thinks pending; fragment reads are
+//    asm too (lds_read_*_async) and retired by explicit lgkmcnt waits.
+// Row image per slot: row r at r*64 B, 16-B chunk c at c ^ (2 * bit2(r))
+// (conflict-free for the 16x16x32 fragment reads' ds_read_b128 lane groups);
+// the NN B operand keeps the column image of the 256 kernel (512-B k rows).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int GS_KS = 32;                    // k-step per LDS slot
+constexpr int GS_OP = G2 * GS_KS * 2;        // 16 KiB per operand per slot
+constexpr int GS_SLOT = 2 * GS_OP;           // 32 KiB
+
+__device__ __forceinline__ uint32_t lds_u32(const char* p) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  return (uint32_t)(uintptr_t)((lds_char*)p);
+}
+
+// 16 B per lane from sbase + voff into LDS [lds_base + 16 * lane): the
+// global address is an SGPR base plus a 32-bit per-lane VGPR offset (one VGPR
+// per DMA instead of a 64-bit pointer); M0 carries the wave-uniform LDS base,
+// set and restored inside the statement.
+__device__ __forceinline__ void glds16_asm(const void* sbase, uint32_t voff, uint32_t lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_base)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched (gfx9 field layout)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | 0x70 | 0xF00 | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void gs_bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ uint32_t gs_swz(int r) { return (uint32_t)(2 * ((r >> 2) & 1)); }
+
+__device__ __forceinline__ const void* sgpr_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// One k-step (32 deep) of A and B into a slot: 32 DMA instructions of 1 KiB,
+// eight per loader wave (lw = 0..3): piece t < 4 is A rows 16 (4 lw + t) ..,
+// piece t >= 4 the matching B piece.  At / Bt: the tile's operand bases at
+// this k-step (wave-uniform).
+template <bool BKC>
+__device__ __forceinline__ void gs_piece(int t, uint32_t slot_lds, const bf16* At, long lda, const bf16* Bt,
+                                         long ldb, int lw, int lane) {
+  const int c = lw * 4 + (t & 3);
+  if (t < 4) {  // 16 rows of 64 B
+    const int row = c * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ (int)gs_swz(row);
+    glds16_asm(sgpr_ptr(At), (uint32_t)((row * lda + lc * 8) * 2),
+               (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + c * 1024));
+    return;
+  }
+  uint32_t off;
+  if (BKC) {
+    const int row = c * 16 + (lane >> 2);
+    const int lc = (lane & 3) ^ (int)gs_swz(row);
+    off = (uint32_t)((row * ldb + lc * 8) * 2);
+  } else {  // 2 k-rows of 256 columns (512 B each)
+    const int k = c * 2 + (lane >> 5);
+    const int lc = (lane & 31) ^ (2 * (int)col_swz(k));
+    off = (uint32_t)((k * ldb + lc * 8) * 2);
+  }
+  glds16_asm(sgpr_ptr(Bt), off, (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + GS_OP + c * 1024));
+}
+template <bool BKC>
+__device__ __forceinline__ void gs_issue(uint32_t slot_lds, const bf16* At, long lda, const bf16* Bt,
+                                         long ldb, int lw, int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) gs_piece<BKC>(t, slot_lds, At, lda, Bt, ldb, lw, lane);
+}
+
+// Epilogue LDS map: eight 32-row passes through fp32 staging rows at 0; the
+// residual / gate rows X of a pass DMA'd one pass ahead into XA (even passes;
+// beyond the four k-step slots, so X(0) loads during the k-loop) or XB (odd,
+// after the staging rows); the bias row (1 KiB) beside XA.
+// The staging rows, XB and the two OUT buffers live in slots 2-3: slots 0-1
+// take the NEXT tile's first two k-steps while this tile's epilogue runs.
+constexpr int GS_EPR = 32;                          // rows per epilogue pass
+constexpr int GS_XA = 4 * GS_SLOT;                  // 128 KiB
+constexpr int GS_BIAS = GS_XA + GS_EPR * 512;       // 144 KiB
+constexpr int GS_EP = 2 * GS_SLOT;                  // 64 KiB: 32 fp32 rows of 1 KiB
+constexpr int GS_XB = GS_EP + GS_EPR * 1024;        // 96 KiB
+constexpr int GS_OUT = GS_XB + GS_EPR * 512;        // 112 KiB: 2 x [16][512 B] bf16
+static_assert(GS_OUT + 2 * 16 * 512 == 4 * GS_SLOT, "epilogue region = slots 2-3");
+static_assert(GS_BIAS + 1024 <= G2_LDS, "LDS budget");
+// fp32 staging element (row, col): 1-KiB rows, column bit 4 flipped on rows
+// with bit 2 set (the owners' lanes l and l + 16 write rows 4 apart)
+__device__ __forceinline__ int gs_ep_idx(int row, int col) { return row * 256 + (col ^ (((row >> 2) & 1) << 4)); }
+
+// 32 rows x 256 columns of the epilogue operand X into an LDS slot
+// [32][512 B]: four 1-KiB DMA instructions per loader wave.  Xt: X at the
+// pass's (r0, c0), wave-uniform.
+__device__ __forceinline__ void gs_xload(uint32_t dst_lds, const bf16* Xt, long ld, int lw, int lane) {
+  const void* sx = sgpr_ptr(Xt);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int chunk = lw * 4 + t;  // 2 rows per KiB
+    const int row = chunk * 2 + (lane >> 5);
+    glds16_asm(sx, (uint32_t)((row * ld + (lane & 31) * 8) * 2),
+               (uint32_t)__builtin_amdgcn_readfirstlane(dst_lds + chunk * 1024));
+  }
+}
+// The tile's 256 bias floats (1 KiB) into LDS: one DMA instruction (every
+// loader wave issues it, so their vmcnt bookkeeping stays uniform).
+__device__ __forceinline__ void gs_bias_load(uint32_t dst_lds, const float* bt, int lane) {
+  glds16_asm(sgpr_ptr(bt), (uint32_t)(lane * 16), dst_lds);
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_b128_off(uint32_t a) {
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return __builtin_bit_cast(bf16x8, r);
+}
+template <int OFF>
+__device__ __forceinline__ bf16x4 lds_tr16_off(uint32_t a) {
+  i16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return __builtin_bit_cast(bf16x4, r);
+}
+
+// The 12 fragment reads of one k-step: 8 A (rows wm*128 + 16 i) and 4 B
+// (columns wn*64 + 16 q), with immediate offsets off one or four base VGPRs.
+template <bool BKC>
+__device__ __forceinline__ void gs_frags(uint32_t slot_lds, int wm, int wn, int lane, bf16x8 (&af)[8],
+                                         bf16x8 (&bfr)[4]) {
+  const int g = lane >> 4, c16 = lane & 15;
+  const uint32_t ab = slot_lds + wm * 8192 + c16 * 64 + ((g ^ gs_swz(c16)) << 4);
+  if constexpr (BKC) {
+    const uint32_t bb = slot_lds + GS_OP + wn * 4096 + c16 * 64 + ((g ^ gs_swz(c16)) << 4);
+    bfr[0] = lds_b128_off<0>(bb);
+    bfr[1] = lds_b128_off<1024>(bb);
+    bfr[2] = lds_b128_off<2048>(bb);
+    bfr[3] = lds_b128_off<3072>(bb);
+  } else {
+    const int qq = c16 >> 2, p = c16 & 3;
+    const int k0 = 8 * g + qq;
+    const uint32_t cs4 = 4 * col_swz(k0);
+    const uint32_t kb = slot_lds + GS_OP + k0 * 512;
+#define GS_BNN(Q)                                                                  \
+    {                                                                              \
+      const uint32_t a = kb + (((uint32_t)(wn * 16 + (Q) * 4 + p) ^ cs4) << 3);   \
+      bfr[Q] = cat4(lds_tr16_off<0>(a), lds_tr16_off<2048>(a));                   \
+    }
+    GS_BNN(0) GS_BNN(1) GS_BNN(2) GS_BNN(3)
+#undef GS_BNN
+  }
+  af[0] = lds_b128_off<0>(ab);
+  af[1] = lds_b128_off<1024>(ab);
+  af[2] = lds_b128_off<2048>(ab);
+  af[3] = lds_b128_off<3072>(ab);
+  af[4] = lds_b128_off<4096>(ab);
+  af[5] = lds_b128_off<5120>(ab);
+  af[6] = lds_b128_off<6144>(ab);
+  af[7] = lds_b128_off<7168>(ab);
+}
+}  // namespace
+
+template <bool BKC>
+__global__ __launch_bounds__(512, 1) void gemm256s_bf16_kernel(int M, int N, int K,
+                                                               const bf16* __restrict__ A, long lda,
+                                                               const bf16* __restrict__ B, long ldb,
+                                                               GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3, lw = wave & 3;
+  const bool loader = wm == 1;  // waves 4-7: every DMA; waves 0-3: every store
+  const int nbm = M / G2, nbn = N / G2;
+  const int nwg = nbm * nbn;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  const int nk = K / GS_KS;  // host: nk >= 4
+  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);
+  const long ldx = e.residual ? e.ldr : e.ldg;
+  const uint32_t lds0 = lds_u32(smem);
+  const int g = lane >> 4, c16 = lane & 15;
+  constexpr int EP_LD = G2 + 4;
+
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // e.dbg: tiles 0 and 1, 4 stamps each
+  int tcount = 0;
+  for (int jj = braw >> 3; jj < xcount; jj += pstride, ++tcount) {
+    const int wgid = xstart + jj;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int m0 = (first_m + within % gsz) * G2, n0 = (within / gsz) * G2;
+    const bool stamp = e.dbg != nullptr && tcount < 2;
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[0] = t_; else st[4] = t_; }
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // operand bases of this tile; k-step k adds k * 32 columns (A, NT B) or
+    // k * 32 rows (NN B)
+    const bf16* At = A + (long)m0 * lda;
+    const bf16* Bt = BKC ? B + (long)n0 * ldb : B + n0;
+    const long bstep = BKC ? GS_KS : (long)GS_KS * ldb;
+
+    // prologue: k-steps 0..2 in flight, k-step 0 landed before the first
+    // barrier (after the first tile, k-steps 0 and 1 were issued during the
+    // previous tile's epilogue)
+    if (loader) {
+      if (tcount == 0) {
+        gs_issue<BKC>(lds0 + 0 * GS_SLOT, At, lda, Bt, ldb, lw, lane);
+        gs_issue<BKC>(lds0 + 1 * GS_SLOT, At + GS_KS, lda, Bt + bstep, ldb, lw, lane);
+      }
+      gs_issue<BKC>(lds0 + 2 * GS_SLOT, At + 2 * GS_KS, lda, Bt + 2 * bstep, ldb, lw, lane);
+      vm_wait<16>();
+    }
+    gs_bar();
+    if (loader) gs_bar();  // the lagging half: one barrier behind from here
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[1] = t_; else st[5] = t_; }
+
+    for (int j = 0; j < nk; ++j) {
+      // R(j): fragment reads of slot j & 3; a loader issues the B half of
+      // k-step j+3 (into the slot k-step j-1 left: every wave retired its
+      // reads of it before its previous M phase) and waits for k-step j+1.
+      // Issue order per loader: B(t) in R(t-3), A(t) in M(t-3).
+      bf16x8 bfr[4], af[8];
+      gs_frags<BKC>(lds0 + (j & 3) * GS_SLOT, wm, wn, lane, af, bfr);
+      const bool do_k = loader && j + 3 < nk;
+      const uint32_t kslot = lds0 + ((j + 3) & 3) * GS_SLOT;
+      const bf16* Aj = At + (long)(j + 3) * GS_KS;
+      const bf16* Bj = Bt + (j + 3) * bstep;
+      if (do_k) {
+#pragma unroll
+        for (int t = 4; t < 8; ++t) gs_piece<BKC>(t, kslot, Aj, lda, Bj, ldb, lw, lane);
+      }
+      if (loader) {
+        if (j + 3 < nk) {
+          vm_wait<12>();  // k-step j+1 landed (B, A of j+2 and B of j+3 fly)
+        } else if (j + 3 == nk) {
+          vm_wait<8>();
+        } else if (j + 2 == nk) {  // k-step nk-1 landed; bias / X(0) may fly on
+          if (xsrc && e.bias) vm_wait<5>();
+          else if (xsrc) vm_wait<4>();
+          else if (e.bias) vm_wait<1>();
+          else vm_wait<0>();
+        }
+      }
+      gs_bar();
+      // M(j): 32 MFMAs; a loader slips the A half of k-step j+3 in behind
+      // every 8 of them (an LDS-DMA piece costs ~60-185 issue cycles: all
+      // eight in one phase stretched it past the partner's 32 MFMAs)
+      lds_tr_retire(af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] = mfma16(af[i], bfr[q], acc[i][q]);
+        if ((i & 1) && do_k) {
+          __builtin_amdgcn_sched_barrier(0);
+          gs_piece<BKC>(i >> 1, kslot, Aj, lda, Bj, ldb, lw, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (loader && j + 3 == nk) {
+        // the epilogue's bias row and first X rows, beyond the four slots
+        // (the bias through LDS: a register load would be a vmcnt wait
+        // hipcc places itself, on the storers' outstanding stores)
+        if (e.bias) gs_bias_load(lds0 + GS_BIAS, e.bias + n0, lane);
+        if (xsrc) gs_xload(lds0 + GS_XA, xsrc + (long)m0 * ldx + n0, ldx, lw, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      gs_bar();
+    }
+    if (!loader) gs_bar();  // realign the halves
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[2] = t_; else st[6] = t_; }
+
+    // ---- epilogue: eight 32-row passes through fp32 LDS staging ---------
+    // The owning half (rows 128 wm .. +127) stages its accumulators; all 512
+    // threads apply bias / ReLU / dropout / residual or gate to 2 items of 8
+    // columns; the storers store theirs, the loaders hand theirs to the
+    // storers as bf16 through OUT (stored one pass later): loaders never
+    // store, so their vmcnt holds DMAs only.  The loaders first issue the
+    // next tile's k-steps 0 and 1 (slots 0-1), which land under this
+    // epilogue, then stream X one pass ahead.
+    const int jn = jj + pstride;
+    const bool has_next = jn < xcount;
+    if (loader && has_next) {
+      const int wn2 = xstart + jn;
+      const int grp2 = wn2 / (GM * nbn);
+      const int gsz2 = min(nbm - grp2 * GM, GM);
+      const int win2 = wn2 % (GM * nbn);
+      const int m1 = (grp2 * GM + win2 % gsz2) * G2, n1 = (win2 / gsz2) * G2;
+      const bf16* At1 = A + (long)m1 * lda;
+      const bf16* Bt1 = BKC ? B + (long)n1 * ldb : B + n1;
+      if (xsrc)  // X(1) ahead of them: its wait then passes over them
+        gs_xload(lds0 + GS_XB, xsrc + (long)(m0 + GS_EPR) * ldx + n0, ldx, lw, lane);
+      gs_issue<BKC>(lds0 + 0 * GS_SLOT, At1, lda, Bt1, ldb, lw, lane);
+      gs_issue<BKC>(lds0 + 1 * GS_SLOT, At1 + GS_KS, lda, Bt1 + bstep, ldb, lw, lane);
+    } else if (loader && xsrc) {
+      gs_xload(lds0 + GS_XB, xsrc + (long)(m0 + GS_EPR) * ldx + n0, ldx, lw, lane);
+    }
+    float* ep = reinterpret_cast<float*>(smem + GS_EP);
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int ch = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      if (loader) {  // X(pass) (and at pass 0 the bias) landed
+        if (xsrc) {
+          if (pass >= 1 && pass < 7)  // X(pass+1) into the slot X(pass-1) left
+            gs_xload(lds0 + (((pass + 1) & 1) ? GS_XB : GS_XA),
+                     xsrc + (long)(m0 + GS_EPR * (pass + 1)) * ldx + n0, ldx, lw, lane);
+          if (pass <= 1) {
+            if (has_next) vm_wait<20>();
+            else vm_wait<4>();
+          } else if (pass < 7) {
+            vm_wait<4>();
+          } else {
+            vm_wait<0>();
+          }
+        } else if (pass == 0 && e.bias) {
+          if (has_next) vm_wait<16>();
+          else vm_wait<0>();
+        }
+      }
+      if (wm == (pass >> 2)) {  // fragment rows i = 2 (pass & 3) + ii
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int i = 2 * (pass & 3) + ii;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[gs_ep_idx(ii * 16 + 4 * g + r, wn * 64 + q * 16 + c16)] = acc[i][q][r];
+        }
+      }
+      smer_lds_barrier();  // staging rows written, X(pass) and the bias landed
+      if (pass == 0 && e.bias) {
+        const float* bl = reinterpret_cast<const float*>(smem + GS_BIAS) + ch * 8;
+        const float4 b0 = *reinterpret_cast<const float4*>(bl);
+        const float4 b1 = *reinterpret_cast<const float4*>(bl + 4);
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      }
+      // storers: the loaders' items of the previous pass (bf16 in OUT)
+      if (!loader && pass >= 1) {
+        const char* ob = smem + GS_OUT + ((pass - 1) & 1) * 8192;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int lr = (tid >> 5) + 8 * c;  // 0..15 -> pass rows 8..15, 24..31
+          const int row = (lr & 7) + 8 + 16 * (lr >> 3);
+          const bf16x8 o = *reinterpret_cast<const bf16x8*>(ob + lr * 512 + ch * 16);
+          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)(m0 + (pass - 1) * GS_EPR + row) * e.ldc + n0 + ch * 8) = o;
+        }
+      }
+      const char* xs = smem + ((pass & 1) ? GS_XB : GS_XA);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int row = (tid >> 5) + 16 * c;  // storers rows 0..7, 16..23; loaders 8..15, 24..31
+        const int grow = m0 + pass * GS_EPR + row, gcol = n0 + ch * 8;
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(ep + gs_ep_idx(row, ch * 8));
+        const float4 b = *reinterpret_cast<const float4*>(ep + gs_ep_idx(row, ch * 8) + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + bv[k];
+        if (e.relu) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+        }
+        if (e.drop_thr)
+          smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
+        if (xsrc) {
+          const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
+          if (e.residual) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += (float)xv[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (float)xv[k] > 0.f ? v[k] * e.gate_scale : 0.f;
+          }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+        if (!loader) {
+          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+        } else {
+          const int lr = (row & 7) + 8 * (row >> 4);
+          *reinterpret_cast<bf16x8*>(smem + GS_OUT + (pass & 1) * 8192 + lr * 512 + ch * 16) = o;
+        }
+      }
+      smer_lds_barrier();  // staging, X(pass) and OUT(pass - 1) read before they are rewritten
+    }
+    if (!loader) {  // the loaders' items of the last pass
+      const char* ob = smem + GS_OUT + 8192;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int lr = (tid >> 5) + 8 * c;
+        const int row = (lr & 7) + 8 + 16 * (lr >> 3);
+        const bf16x8 o = *reinterpret_cast<const bf16x8*>(ob + lr * 512 + ch * 16);
+        *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)(m0 + 7 * GS_EPR + row) * e.ldc + n0 + ch * 8) = o;
+      }
+    }
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[3] = t_; else st[7] = t_; }
+  }
+  if (e.dbg && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e.dbg[((long)blockIdx.x * 8 + wave) * 8 + k] = st[k];
+  }
+}
+
+// phase stamps of the staggered kernel (diagnostics; tools/gemm256s_phases.py)
+static unsigned long long* g_gemm_dbg = nullptr;
+extern "C" int smer_gemm_debug_stamps(void* buf) {
+  g_gemm_dbg = (unsigned long long*)buf;
+  return SMER_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradients on the 256x256 tile: dW (+)= dY^T X with K = tokens, both
 // operands M/N-contiguous (column images, transposing fragment reads).  Half
 // the L2->CU bytes per flop of the 128x128 kernel and twice the MFMA work per
@@ -1256,6 +1723,13 @@ static bool smer_gemm256_enabled() {
   return !(e && e[0] == '0');
 }
 
+// SMER_GEMM256S=0 keeps the whole-tile bf16-output shapes on the two-stage
+// 256x256 kernel instead of the staggered one (read per call: A/B in-process)
+static bool smer_gemm256s_enabled() {  // opt-in until it beats the two-stage kernel
+  const char* e = getenv("SMER_GEMM256S");
+  return e && e[0] == '1';
+}
+
 // SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests)
 static bool smer_gemm64_enabled() {
   static int v = -1;
@@ -1406,6 +1880,25 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   // large-M forward / dgrad: 256x256 tiles when they fill the chip
   if (AK && !rowsum && K % G2K == 0 && smer_gemm256_enabled()) {
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
+    // whole tiles with a bf16 output: the staggered kernel
+    if (t2 >= smer_g256_min_tiles() && smer_gemm256s_enabled() && M % G2 == 0 && N % G2 == 0 &&
+        K % GS_KS == 0 && K / GS_KS >= 4 && e.vec && e.C && !e.Cf && !e.kv && !e.q8 &&
+        !(e.residual && e.gate)) {
+      static bool attr_s = false;
+      if (!attr_s) {
+        hipFuncSetAttribute((const void*)gemm256s_bf16_kernel<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+        hipFuncSetAttribute((const void*)gemm256s_bf16_kernel<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+        attr_s = true;
+      }
+      const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
+      GemmEpi ed = e;
+      ed.dbg = g_gemm_dbg;
+      hipLaunchKernelGGL(gemm256s_bf16_kernel<BKC>, dim3(grid), dim3(512), G2_LDS, s,
+                         M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, ed);
+      return;
+    }
     if (t2 >= smer_g256_min_tiles()) {
       const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
       static bool attr_set = false;  // > 64 KiB dynamic LDS must be opted into
@@ -1497,45 +1990,50 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   }
 }
 // Skinny f32 NT GEMM (parity-mode decode steps: M = 2 rows per request).
-// The 64x64 tile kernel runs N / 64 workgroups there (8 for a d = 512
-// Linear), each re-reading a 64-row weight strip: the batch-1 fp32 decode
-// step took 3.2 ms.  Here a workgroup owns 16 output columns x up to 16
-// rows; its 4 waves split K, lane (c16, kq) streams W[col][k + 4 kq .. + 3]
-// with 16-B loads (the 16 columns x 16 k of a wave step: 1 KiB), four
-// k-steps in flight.  Partial dot products reduced over kq by shuffles and
-// over the waves through LDS in fixed order (deterministic).
-constexpr int SKF_BN = 16, SKF_BM = 16, SKF_NW = 4, SKF_UNR = 4;
+// Latency-bound: at M = 2 the step streams the fp32 weights (14.7 MB per C2
+// decoder layer) with nothing else to do, so what counts is how many bytes
+// are in flight at once.  A workgroup owns 4 output columns x up to 16 rows;
+// lane (column lane >> 4, k-chunk lane & 15) of a wave step reads
+// W[col][k + 4 (lane & 15) .. + 3] (4 columns x 64 k = 1 KiB per wave step),
+// the 4 waves take the steps round-robin, 8 steps per wave in flight: a
+// K = 2048 Linear issues all of its 32 KiB per workgroup up front, and the
+// grid has N / 4 workgroups (128-512 at C2; round 3's 16-column strips ran
+// N / 16 with 16 KiB in flight each).  Partial sums reduced over the 16
+// lanes of a column by xor shuffles and over the waves through LDS, in fixed
+// order (deterministic; a row's sum never depends on the other rows).
+constexpr int SKF_BN = 4, SKF_BM = 16, SKF_NW = 4, SKF_UNR = 8;
 __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_f32_kernel(int M, int N, int K,
                                                                       const float* __restrict__ A, long lda,
                                                                       const float* __restrict__ B, long ldb,
                                                                       GemmEpi e) {
-  __shared__ float red[SKF_NW][SKF_BM][SKF_BN + 1];
+  __shared__ float red[SKF_NW][SKF_BM][SKF_BN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c16 = lane & 15, kq = lane >> 4;
+  const int cq = lane >> 4, kq = lane & 15;
   const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
-  const int col = n0 + c16;
+  const int col = n0 + cq;
   const bool colok = col < N;
   const int mrows = min(SKF_BM, M - m0);
   const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  const float* a0 = A + (long)m0 * lda + 4 * kq;
   float acc[SKF_BM];
 #pragma unroll
   for (int r = 0; r < SKF_BM; ++r) acc[r] = 0.f;
-  const int nsteps = (K + 15) / 16;  // 16 k per wave step (4 lanes x 4)
+  const int nsteps = (K + 63) / 64;  // 64 k per wave step (16 lanes x 4)
   for (int s0 = wave; s0 < nsteps; s0 += SKF_NW * SKF_UNR) {
     float4 b[SKF_UNR];
 #pragma unroll
     for (int u = 0; u < SKF_UNR; ++u) {
-      const int k = (s0 + u * SKF_NW) * 16;
+      const int k = (s0 + u * SKF_NW) * 64;
       b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < SKF_UNR; ++u) {
-      const int k = (s0 + u * SKF_NW) * 16 + 4 * kq;
-      if (k >= K) continue;
+      const int k = (s0 + u * SKF_NW) * 64;
+      if (k + 4 * kq >= K) continue;
 #pragma unroll
       for (int r = 0; r < SKF_BM; ++r) {
         if (r < mrows) {
-          const float4 a = *reinterpret_cast<const float4*>(A + (long)(m0 + r) * lda + k);
+          const float4 a = *reinterpret_cast<const float4*>(a0 + (long)r * lda + k);
           acc[r] = fmaf(a.x, b[u].x, acc[r]);
           acc[r] = fmaf(a.y, b[u].y, acc[r]);
           acc[r] = fmaf(a.z, b[u].z, acc[r]);
@@ -1544,15 +2042,19 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_f32_kernel(int M, int
       }
     }
   }
-  // sum the four kq lane groups (lanes c16, +16, +32, +48), then the waves
+  // sum the 16 k-chunk lanes of each column, then the waves
 #pragma unroll
   for (int r = 0; r < SKF_BM; ++r) {
-    acc[r] += __shfl_xor(acc[r], 16, 64);
-    acc[r] += __shfl_xor(acc[r], 32, 64);
+    if (r < mrows) {
+      acc[r] += __shfl_xor(acc[r], 1, 64);
+      acc[r] += __shfl_xor(acc[r], 2, 64);
+      acc[r] += __shfl_xor(acc[r], 4, 64);
+      acc[r] += __shfl_xor(acc[r], 8, 64);
+    }
   }
   if (kq == 0) {
 #pragma unroll
-    for (int r = 0; r < SKF_BM; ++r) red[wave][r][c16] = acc[r];
+    for (int r = 0; r < SKF_BM; ++r) red[wave][r][cq] = acc[r];
   }
   __syncthreads();
   if (tid < SKF_BM * SKF_BN) {

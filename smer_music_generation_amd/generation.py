@@ -68,7 +68,25 @@ def weighted_sampling(probs):
         raise TypeError("weighted_sampling expects float64 probabilities")
     probs /= np.add.accumulate(probs)[-1]
     sorted_index = np.argsort(probs)[::-1]
-    return np.random.choice(sorted_index, size=1, p=probs[sorted_index])[0]
+    return _choice1(sorted_index, probs[sorted_index])
+
+
+def _choice1(a, p):
+    """np.random.choice(a, size=1, p=p)[0] on the global RandomState, without
+    its argument checks (a third of the per-token host time): NumPy's legacy
+    `RandomState.choice` with replacement draws ONE `random_sample` and
+    returns a[searchsorted(cdf / cdf[-1], u, side='right')], so the same
+    uniform gives the same index and leaves the same generator state.  Any
+    input its checks would reject (a negative or NaN entry, a sum off 1)
+    goes to np.random.choice itself, so the errors are NumPy's own
+    (tests/test_sampling.py compares the two on seeded streams)."""
+    cdf = np.cumsum(p)
+    total = cdf[-1]
+    if not (abs(total - 1.0) <= 1e-9) or not (p >= 0.0).all():
+        return np.random.choice(a, size=1, p=p)[0]
+    cdf /= total
+    u = np.random.random_sample(1)
+    return a[cdf.searchsorted(u, side='right')][0]
 
 
 _FLAG_NAMES = ("no_pitch", "no_duration", "no_rest", "no_whole_duration", "no_eos",
@@ -406,11 +424,14 @@ class _Precision:
 
 def generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
                    bars_to_generate, *, greedy=False, use_kv_cache=True, stats=None,
-                   precision="fp32"):
+                   precision="fp32", warm=True):
     """`generation.py:468-696`.  Returns (restored '<U9' tokens,
     mask_track_names, mask_bar_names) or None (nothing masked / on error,
     after printing it, as the reference does).  `stats` (a dict, opt-in)
     receives the number of decode steps (= tokens drawn).
+    warm: decode on this model's cached batch-1 session (KV caches and the
+    captured step graph kept across calls, as in generation_batch); False
+    builds a private session freed after the call.
     precision: arithmetic of this call's decode.  "fp32" (default) gives
     the reference's token ids bit for bit (north_star: bit-exact greedy ids;
     sampled ids are the same draws of the same numpy stream) whatever
@@ -419,11 +440,12 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
     near-ties); the batched serving API `generation_batch` keeps None."""
     with _Precision(model, precision):
         return _generation_all(model, events, device, vocab, logger, all_controls,
-                               tracks_to_generate, bars_to_generate, greedy, use_kv_cache, stats)
+                               tracks_to_generate, bars_to_generate, greedy, use_kv_cache, stats,
+                               warm)
 
 
 def _generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
-                    bars_to_generate, greedy, use_kv_cache, stats):
+                    bars_to_generate, greedy, use_kv_cache, stats, warm=True):
     try:
         src, mtn, mbn, target, no_whole = _prepare(events, vocab, tracks_to_generate,
                                                    bars_to_generate)
@@ -434,7 +456,11 @@ def _generation_all(model, events, device, vocab, logger, all_controls, tracks_t
         with torch.no_grad():
             steps = 0
             if use_kv_cache:
-                sess = DecodeSession(model, 1, len(src), max(128, 100 * st.n_masks + 8))
+                # the warm batch-1 session of this model and precision: KV
+                # caches, step buffers and the captured step graph persist
+                # across plugin calls (same rules as generation_batch's)
+                sess = _batch_session(model, 1, len(src), max(128, 100 * st.n_masks + 8), None,
+                                      warm=warm)
                 sess.prefill([0], [src])
                 fed = 0
                 while not st.done:

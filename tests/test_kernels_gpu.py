@@ -156,6 +156,57 @@ def test_gemm256_streamed_epilogue_gate(M, N, K, bk):
     assert rel_err(C, base + G.float()) < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K,bk,epi", [
+    (8192, 2048, 512, True, "bias_relu_drop"), (8192, 2048, 512, False, "gate"),
+    (32768, 512, 2048, True, "bias_residual"), (16384, 1536, 512, True, "bias"),
+    (16384, 512, 1536, False, "residual"), (8192, 512, 2048, False, "none"),
+    (12288, 768, 128, True, "bias_residual")])
+def test_gemm256s_matches_two_stage_kernel(monkeypatch, M, N, K, bk, epi):
+    """The staggered 256x256 kernel (four k-step slots, loader / storer wave
+    roles, 32-row epilogue passes) against the two-stage 256x256 kernel it
+    replaces (SMER_GEMM256S=0): same k order and epilogue arithmetic, so the
+    outputs are bit-identical; and against fp32.  Shapes: >= 256 whole tiles
+    (one per CU and more: the persistent tile loop), K from 4 k-steps up."""
+    O = ops()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(dev).to(torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(dev).to(torch.bfloat16)
+    Wm = W if bk else W.t().contiguous()
+    X = torch.randn(M, N, generator=g).to(dev).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(dev)
+    kw = {}
+    if "bias" in epi:
+        kw["bias"] = bias
+    if "relu" in epi:
+        kw["relu"] = True
+    if "drop" in epi:
+        kw["drop_p"], kw["seed"] = 0.1, 11
+    if "residual" in epi:
+        kw["residual"] = X
+    if "gate" in epi:
+        kw["gate"], kw["gate_scale"] = X, 1.25
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SMER_GEMM256S", flag)
+        C = torch.full((M, N), float("nan"), device=dev, dtype=torch.bfloat16)
+        O.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)
+        outs[flag] = C
+    torch.cuda.synchronize()
+    assert torch.equal(outs["1"], outs["0"]), (outs["1"] - outs["0"]).abs().max()
+    base = A.float() @ W.float().t()
+    ref = base + (bias if "bias" in epi else 0)
+    if "relu" in epi:
+        ref = torch.relu(ref)
+    if "drop" in epi:
+        keep = torch.from_numpy(keep_mask(11, 0.1, M, N)).to(dev)
+        ref = torch.where(keep, ref * drop_scale(0.1), torch.zeros_like(ref))
+    if "residual" in epi:
+        ref = ref + X.float()
+    if "gate" in epi:
+        ref = torch.where(X.float() > 0, ref * 1.25, torch.zeros_like(ref))
+    assert rel_err(outs["1"], ref) < 2e-2
+
+
 def test_gemm_identity_asymmetric():
     O = ops()
     n = 128
@@ -169,7 +220,8 @@ def test_gemm_identity_asymmetric():
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,N,K", [(192, 256, 128), (640, 264, 136), (40, 264, 136),
-                                   (64, 512, 2048), (130, 264, 1040)])
+                                   (64, 512, 2048), (130, 264, 1040), (2, 309, 512), (2, 512, 2048),
+                                   (17, 1544, 520)])
 def test_gemm_epilogue(dtype, M, N, K):
     """Skinny (M <= 256) and tiled kernels, incl. N and K tails."""
     O = ops()
