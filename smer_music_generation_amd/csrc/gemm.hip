@@ -1478,6 +1478,227 @@ __global__ __launch_bounds__(512, 1) void gemm256_wgrad_kernel(int M, int N, int
 }
 
 // ---------------------------------------------------------------------------
+// Staggered 256x256 weight-gradient kernel: dW (+)= dY^T X with both operands
+// column images (K = tokens), the k-loop schedule of gemm256s_bf16_kernel
+// (four 32-deep slots, three k-steps ahead, halves one barrier apart, waves
+// 4-7 issue every DMA, waves 0-3 every store) on the split-K work items of
+// gemm256_wgrad_kernel (slice, tile).  Fragments of both operands are
+// transposing reads (ds_read_b64_tr_b16) of 512-B k rows; the fused bias
+// gradient sums two A fragments per wave per k-step (v_dot2c, as there).
+// Output fp32: a split-K slab, or dW (+)= alpha * acc unsplit.
+// ---------------------------------------------------------------------------
+namespace {
+// piece t < 4: A k-rows 2c, 2c+1 (c = 4 lw + t), t >= 4: the B ones
+__device__ __forceinline__ void gsw_piece(int t, uint32_t slot_lds, const bf16* At, long lda, const bf16* Bt,
+                                          long ldb, int lw, int lane) {
+  const int c = lw * 4 + (t & 3);
+  const int k = c * 2 + (lane >> 5);
+  const int lc = (lane & 31) ^ (2 * (int)col_swz(k));
+  if (t < 4)
+    glds16_asm(sgpr_ptr(At), (uint32_t)((k * lda + lc * 8) * 2),
+               (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + c * 1024));
+  else
+    glds16_asm(sgpr_ptr(Bt), (uint32_t)((k * ldb + lc * 8) * 2),
+               (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + GS_OP + c * 1024));
+}
+__device__ __forceinline__ void gsw_issue(uint32_t slot_lds, const bf16* At, long lda, const bf16* Bt, long ldb,
+                                          int lw, int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) gsw_piece(t, slot_lds, At, lda, Bt, ldb, lw, lane);
+}
+// 8 A fragments (rows wm*128 + 16 i) and 4 B (columns wn*64 + 16 q) of one
+// k-step, 24 transposing reads; aoff / boff: the lane's byte offsets in a slot
+__device__ __forceinline__ void gsw_frags(uint32_t slot_lds, const uint32_t (&aoff)[8], const uint32_t (&boff)[4],
+                                          bf16x8 (&af)[8], bf16x8 (&bfr)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t a = slot_lds + boff[q];
+    bfr[q] = cat4(lds_tr16_off<0>(a), lds_tr16_off<2048>(a));
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t a = slot_lds + aoff[i];
+    af[i] = cat4(lds_tr16_off<0>(a), lds_tr16_off<2048>(a));
+  }
+}
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void gemm256s_wgrad_kernel(int M, int N, int K, const bf16* __restrict__ A,
+                                                                long lda, const bf16* __restrict__ B, long ldb,
+                                                                GemmEpi e, int ksplit, int kchunk,
+                                                                float* __restrict__ slabs,
+                                                                float* __restrict__ rowsum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3, lw = wave & 3;
+  const bool loader = wm == 1;
+  const int nbm = M / G2, nbn = N / G2;
+  const int ntiles = nbm * nbn;
+  const int nwg = ntiles * ksplit;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  const uint32_t lds0 = lds_u32(smem);
+  const int g = lane >> 4, c16 = lane & 15;
+  uint32_t aoff[8], boff[4];
+  {
+    const int qq = c16 >> 2, p = c16 & 3;
+    const int k0 = 8 * g + qq;
+    const uint32_t cs4 = 4 * col_swz(k0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) aoff[i] = k0 * 512 + ((((uint32_t)(wm * 32 + i * 4 + p)) ^ cs4) << 3);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) boff[q] = GS_OP + k0 * 512 + ((((uint32_t)(wn * 16 + q * 4 + p)) ^ cs4) << 3);
+  }
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int lin = xstart + jj;
+    const int split = lin / ntiles, wgid = lin % ntiles;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int tn = within / gsz;
+    const int m0 = (first_m + within % gsz) * G2, n0 = tn * G2;
+    const int k_begin = split * kchunk, k_end = min(K, k_begin + kchunk);
+    const int nk = (k_end - k_begin) / GS_KS;  // host: >= 1
+    const bool rsum = rowsum != nullptr && tn == 0;
+    const int wn_s = __builtin_amdgcn_readfirstlane(wn);
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float rs0 = 0.f, rs1 = 0.f;
+    // column images: k-step k adds 32 k-rows
+    const bf16* At = A + (long)k_begin * lda + m0;
+    const bf16* Bt = B + (long)k_begin * ldb + n0;
+    const long astep = (long)GS_KS * lda, bstep = (long)GS_KS * ldb;
+
+    if (loader) {
+      gsw_issue(lds0, At, lda, Bt, ldb, lw, lane);
+      if (nk > 1) gsw_issue(lds0 + GS_SLOT, At + astep, lda, Bt + bstep, ldb, lw, lane);
+      if (nk > 2) gsw_issue(lds0 + 2 * GS_SLOT, At + 2 * astep, lda, Bt + 2 * bstep, ldb, lw, lane);
+      if (nk > 2) vm_wait<16>();
+      else if (nk == 2) vm_wait<8>();
+      else vm_wait<0>();
+    }
+    gs_bar();
+    if (loader) gs_bar();
+
+    for (int j = 0; j < nk; ++j) {
+      bf16x8 bfr[4], af[8];
+      gsw_frags(lds0 + (j & 3) * GS_SLOT, aoff, boff, af, bfr);
+      const bool do_k = loader && j + 3 < nk;
+      const uint32_t kslot = lds0 + ((j + 3) & 3) * GS_SLOT;
+      const bf16* Aj = At + (long)(j + 3) * astep;
+      const bf16* Bj = Bt + (long)(j + 3) * bstep;
+      if (do_k) {
+#pragma unroll
+        for (int t = 4; t < 8; ++t) gsw_piece(t, kslot, Aj, lda, Bj, ldb, lw, lane);
+      }
+      if (loader) {
+        if (j + 3 < nk) vm_wait<12>();
+        else if (j + 3 == nk) vm_wait<8>();
+        else if (j + 2 == nk) vm_wait<0>();
+      }
+      gs_bar();
+      lds_tr_retire(af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] = mfma16(af[i], bfr[q], acc[i][q]);
+        if ((i & 1) && do_k) {
+          __builtin_amdgcn_sched_barrier(0);
+          gsw_piece(i >> 1, kslot, Aj, lda, Bj, ldb, lw, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (rsum) {  // wave wn sums A fragments 2wn, 2wn+1 (rows of its 32)
+        if (wn_s == 0)      { rs0 = rowsum_frag(af[0], rs0); rs1 = rowsum_frag(af[1], rs1); }
+        else if (wn_s == 1) { rs0 = rowsum_frag(af[2], rs0); rs1 = rowsum_frag(af[3], rs1); }
+        else if (wn_s == 2) { rs0 = rowsum_frag(af[4], rs0); rs1 = rowsum_frag(af[5], rs1); }
+        else                { rs0 = rowsum_frag(af[6], rs0); rs1 = rowsum_frag(af[7], rs1); }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      gs_bar();
+    }
+    if (!loader) gs_bar();  // realign the halves (every wave past its last reads)
+
+    if (rsum) {
+      rs0 += __shfl_xor(rs0, 16); rs0 += __shfl_xor(rs0, 32);
+      rs1 += __shfl_xor(rs1, 16); rs1 += __shfl_xor(rs1, 32);
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = m0 + wm * 128 + (2 * wn + j) * 16 + lane;
+          const float v = j ? rs1 : rs0;
+          if (ksplit > 1) rowsum[(long)split * M + row] = v;
+          else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + v * e.alpha;
+        }
+      }
+    }
+    // ---- epilogue: eight 32-row passes through fp32 staging (slots 2-3);
+    // the storers store every item (the loaders' rows 128..255 included)
+    float* ep = reinterpret_cast<float*>(smem + GS_EP);
+    float* slab = ksplit > 1 ? slabs + (long)split * M * N : nullptr;
+    const int ch = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      if (wm == (pass >> 2)) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int i = 2 * (pass & 3) + ii;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              ep[gs_ep_idx(ii * 16 + 4 * g + r, wn * 64 + q * 16 + c16)] = acc[i][q][r];
+        }
+      }
+      smer_lds_barrier();
+      if (!loader) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int row = (tid >> 5) + 8 * c;  // 0..31
+          const long grow = m0 + pass * GS_EPR + row;
+          const int gcol = n0 + ch * 8;
+          float4 a = *reinterpret_cast<const float4*>(ep + gs_ep_idx(row, ch * 8));
+          float4 b = *reinterpret_cast<const float4*>(ep + gs_ep_idx(row, ch * 8) + 4);
+          if (slab) {
+            float* dst = slab + grow * N + gcol;
+            *reinterpret_cast<float4*>(dst) = a;
+            *reinterpret_cast<float4*>(dst + 4) = b;
+          } else {
+            float* dst = e.Cf + grow * e.ldcf + gcol;
+            const float al = e.alpha;
+            a.x *= al; a.y *= al; a.z *= al; a.w *= al;
+            b.x *= al; b.y *= al; b.z *= al; b.w *= al;
+            if (e.accumulate) {
+              const float4 o0 = *reinterpret_cast<const float4*>(dst);
+              const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
+              a.x += o0.x; a.y += o0.y; a.z += o0.z; a.w += o0.w;
+              b.x += o1.x; b.y += o1.y; b.z += o1.z; b.w += o1.w;
+            }
+            *reinterpret_cast<float4*>(dst) = a;
+            *reinterpret_cast<float4*>(dst + 4) = b;
+          }
+        }
+      }
+      smer_lds_barrier();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Skinny bf16 NT GEMM (M <= 256: decode steps, tiny batches).  The 128x128
 // tile kernel would run 4-16 workgroups there; this one gives each
 // workgroup a 64-row x 16-column output strip and splits K over its 8 waves.
@@ -1723,11 +1944,19 @@ static bool smer_gemm256_enabled() {
   return !(e && e[0] == '0');
 }
 
-// SMER_GEMM256S=0 keeps the whole-tile bf16-output shapes on the two-stage
-// 256x256 kernel instead of the staggered one (read per call: A/B in-process)
-static bool smer_gemm256s_enabled() {  // opt-in until it beats the two-stage kernel
+// Whole-tile bf16-output shapes: the staggered kernel where it measured
+// faster than the two-stage one (tools/gemm256s_ab.py, round 4): K >= 1024
+// (C2 FFN2 forward 69.7 vs 73.3 us, FFN1 / QKV dgrads 66.0 / 52.6 vs 71.1 /
+// 56.6, C4 FFN1 dgrad 202 vs 224) and the NN dgrads with N >= 1024 (gated
+// FFN2 dgrad 104.8 vs 116.9); the K = 512 forwards keep the two-stage kernel
+// (FFN1 106.9 vs 101.8, QKV 68.8 vs 68.0: their epilogue, not the k-loop,
+// sets the time).  SMER_GEMM256S=1 / 0 forces it on / off (read per call:
+// A/B in-process).
+static bool smer_gemm256s_enabled(bool bkc, int N, int K) {
   const char* e = getenv("SMER_GEMM256S");
-  return e && e[0] == '1';
+  if (e && e[0] == '1') return true;
+  if (e && e[0] == '0') return false;
+  return K >= 1024 || (!bkc && N >= 1024);
 }
 
 // SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests)
@@ -1778,6 +2007,14 @@ static bool smer_wgrad256_enabled(int M, int N) {
     v = (e && e[0] == '1') ? 1 : (e && e[0] == '0') ? 0 : 2;
   }
   return v == 1 || (v == 2 && (long)M * N >= 1536L * 768);
+}
+// The 256x256 weight gradients on the staggered schedule
+// (gemm256s_wgrad_kernel; tools/bench_wgrad.py c4: 2304x768x65536 249 vs
+// 284 us, 3072x768 326 vs 356, 768x3072 302 vs 334, 768x768 equal);
+// SMER_WGRAD256S=0: the two-stage gemm256_wgrad_kernel (read per call)
+static bool smer_wgrad256s_enabled() {
+  const char* e = getenv("SMER_WGRAD256S");
+  return !(e && e[0] == '0');
 }
 static int smer_wgrad256_depth() {
   static int v = -1;
@@ -1881,7 +2118,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   if (AK && !rowsum && K % G2K == 0 && smer_gemm256_enabled()) {
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
     // whole tiles with a bf16 output: the staggered kernel
-    if (t2 >= smer_g256_min_tiles() && smer_gemm256s_enabled() && M % G2 == 0 && N % G2 == 0 &&
+    if (t2 >= smer_g256_min_tiles() && smer_gemm256s_enabled(BKC, N, K) && M % G2 == 0 && N % G2 == 0 &&
         K % GS_KS == 0 && K / GS_KS >= 4 && e.vec && e.C && !e.Cf && !e.kv && !e.q8 &&
         !(e.residual && e.gate)) {
       static bool attr_s = false;
@@ -1941,6 +2178,17 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
       const long nwg = t2 * split;
       const int grid = nwg > cus ? (int)(cus & ~7L) : (int)nwg;
+      if (smer_wgrad256s_enabled() && M % G2 == 0 && N % G2 == 0 && e.vec) {
+        static bool attr_s = false;
+        if (!attr_s) {
+          hipFuncSetAttribute((const void*)gemm256s_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              4 * GS_SLOT);
+          attr_s = true;
+        }
+        hipLaunchKernelGGL(gemm256s_wgrad_kernel, dim3(grid), dim3(512), 4 * GS_SLOT, s, M, N, K,
+                           (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
+                           split > 1 ? rs_part : rowsum);
+      } else
       hipLaunchKernelGGL(gemm256_wgrad_kernel, dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
                          (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
                          split > 1 ? rs_part : rowsum);

@@ -111,6 +111,34 @@ def test_gemm_wgrad_bias(M, N, K, acc):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,N,K,acc", [(1536, 768, 16384, True), (3072, 768, 8192, False),
+                                       (2304, 768, 32768, True), (4096, 4096, 512, True)])
+def test_gemm256s_wgrad_matches_reference(monkeypatch, M, N, K, acc):
+    """The staggered weight-gradient kernel (SMER_WGRAD256S=1) on the 256x256
+    split-K shapes: dw = dy^T x and db = column sums of dy (split and
+    unsplit, accumulate on / off) against fp32 torch, deterministic, and
+    against the two-stage 256x256 kernel (same k order per slice)."""
+    O = ops()
+    dy = torch.randn(K, M, device=dev).to(torch.bfloat16)
+    x = torch.randn(K, N, device=dev).to(torch.bfloat16)
+    dw0, db0 = torch.randn(M, N, device=dev), torch.randn(M, device=dev)
+    ref_w = dy.float().t() @ x.float() + (dw0 if acc else 0)
+    ref_b = dy.float().sum(0) + (db0 if acc else 0)
+    outs = {}
+    for flag in ("1", "1", "0"):
+        monkeypatch.setenv("SMER_WGRAD256S", flag)
+        dw, db = dw0.clone(), db0.clone()
+        O.linear_wgrad(dy, x, dw, M=M, accumulate=acc, db=db)
+        torch.cuda.synchronize()
+        if flag in outs:
+            assert torch.equal(dw, outs[flag][0]) and torch.equal(db, outs[flag][1])
+        outs[flag] = (dw, db)
+    dw, db = outs["1"]
+    assert rel_err(dw, ref_w) < 2e-3
+    assert rel_err(db, ref_b) < 2e-3
+    assert rel_err(dw, outs["0"][0]) < 1e-5 and rel_err(db, outs["0"][1]) < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K,bk", [(8300, 2056, 512, True), (8192, 2048, 192, False),
                                       (16384, 1536, 1024, True), (8200, 2048, 256, False)])
 def test_gemm256_large_m(M, N, K, bk):

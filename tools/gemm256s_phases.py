@@ -9,6 +9,8 @@ import ctypes
 import os
 import sys
 
+os.environ["SMER_GEMM256S"] = "1"  # the kernel is opt-in
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
