@@ -217,6 +217,21 @@ int smer_linear_decode_ln(int M, int N, int K, const void* Y, long ldy, const fl
                           long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
                           long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
                           int kv_col0, smer_stream_t stream);
+/* fp32 forms of smer_linear_decode / smer_linear_decode_ln (every operand
+ * fp32; M <= 64): the parity-mode decode step of the plugin call, which
+ * replaces the reference's per-token full fp32 recompute
+ * (generation.py:542-545 -> model_generate, generation.py:209-225). */
+int smer_linear_decode_f32(int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                           const float* bias, int relu, const void* residual, long ldr, void* C,
+                           long ldc, float* Cf, long ldcf, void* kv, long kv_row_stride,
+                           long kv_req_stride, const int32_t* kv_req, const int32_t* kv_pos,
+                           int kv_col0, smer_stream_t stream);
+int smer_linear_decode_ln_f32(int M, int N, int K, const void* Y, long ldy, const float* gamma,
+                              const float* beta, float eps, void* X, long ldx, const void* W,
+                              long ldw, const float* bias, int relu, const void* residual,
+                              long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
+                              long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
+                              const int32_t* kv_pos, int kv_col0, smer_stream_t stream);
 /* One greedy grammar step for R requests (generation.py:528-687).
  * logits: fp32 [2R, >=V] rows (request r's last fed token at row 2r+1).
  * state: int32 [R, nst>=9] = pos, flags(sep|cont<<1|pitch<<2|rest<<3), span

@@ -58,6 +58,11 @@ SIGNATURES = {
     "smer_linear_decode_ln": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
                                       c_long, P, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
                                       c_long, P, P, c_int, P]),
+    "smer_linear_decode_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
+                                       P, c_long, P, c_long, P, c_long, c_long, P, P, c_int, P]),
+    "smer_linear_decode_ln_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
+                                          c_long, P, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
+                                          c_long, P, P, c_int, P]),
     "smer_fp8_quantize_workspace": (c_size, []),
     "smer_fp8_quantize": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P]),
     "smer_fp8_quantize_segments": (c_int, [c_int, P, P, P, c_int, P]),

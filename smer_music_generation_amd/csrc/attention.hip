@@ -1062,6 +1062,134 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(int B, int H, int Lq, int Lk
   if (lane == 0) lse[(long)bh * Lq + qi] = sum > 0.f ? mu + logf(sum) : INFINITY;
 }
 
+// fp32 flash forward on the fp32 MFMA (v_mfma_f32_16x16x4_f32: full fp32
+// products and sums, no reduced-precision inputs), D = 64, no dropout: the
+// parity-mode prefill of the plugin call (encoder self-attention over ~1k
+// source tokens: 1.26 ms per layer on attn_fwd_f32's wave-per-query loop)
+// and fp32 training forwards.  A wave owns 16 queries; per 64-key tile it
+// forms S^T = K Q^T (16x16 blocks, keys as rows) so that a lane's four
+// scores of a block (keys 4g + r, query c16) are exactly the A operand of
+// the four P.V MFMAs (key sets {4g + r}), no transposition; the contraction
+// over d runs in lane-group order (MFMA c sums d = 16 g + c over g), so each
+// lane reads 16 consecutive floats of one Q row and one K row.  Online
+// softmax with expf in fp32 (lse = m + log l, as attn_fwd_f32); rows with no
+// visible key give O = 0, lse = +inf.
+__global__ __launch_bounds__(256) void attn_fwd_f32_mfma(int B, int H, int Lq, int Lk,
+                                                         const float* __restrict__ q, long ldq,
+                                                         const float* __restrict__ k, long ldk,
+                                                         const float* __restrict__ v, long ldv,
+                                                         float* __restrict__ o, long ldo,
+                                                         float* __restrict__ lse,
+                                                         const uint8_t* __restrict__ kpm, int causal,
+                                                         float scale) {
+  constexpr int D = 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+  if (q0 >= Lq) return;  // no block-level synchronisation below
+  const int c16 = lane & 15, g = lane >> 4;
+  const int qi = q0 + c16;  // this lane's query (S^T column)
+  float qf[16];
+  {
+    const float4* qr = reinterpret_cast<const float4*>(q + (long)(b * Lq + min(qi, Lq - 1)) * ldq + h * D + 16 * g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 t = qr[i];
+      qf[4 * i] = t.x * scale; qf[4 * i + 1] = t.y * scale; qf[4 * i + 2] = t.z * scale; qf[4 * i + 3] = t.w * scale;
+    }
+  }
+  f32x4 oacc[4];
+#pragma unroll
+  for (int dq = 0; dq < 4; ++dq) oacc[dq] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;  // query qi's running max / sum (same in all 4 g lanes)
+  const uint8_t* kp = kpm ? kpm + (long)b * Lk : nullptr;
+  const int kend = causal ? min(Lk, q0 + 16) : Lk;
+  const float* kb0 = k + (long)b * Lk * ldk + h * D;
+  const float* vb0 = v + (long)b * Lk * ldv + h * D;
+  for (int k0 = 0; k0 < kend; k0 += 64) {
+    f32x4 st[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int key = min(k0 + 16 * kb + c16, Lk - 1);
+      const float4* kr = reinterpret_cast<const float4*>(kb0 + (long)key * ldk + 16 * g);
+      float kf[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4 t = kr[i];
+        kf[4 * i] = t.x; kf[4 * i + 1] = t.y; kf[4 * i + 2] = t.z; kf[4 * i + 3] = t.w;
+      }
+      st[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) st[kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[c], qf[c], st[kb], 0, 0, 0);
+    }
+    // V rows of the four P.V MFMAs per key block: key 16 kb + 4 g + r,
+    // columns 16 dq + c16
+    float vf[4][4][4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* vr = vb0 + (long)min(k0 + 16 * kb + 4 * g + r, Lk - 1) * ldv + c16;
+#pragma unroll
+        for (int dq = 0; dq < 4; ++dq) vf[kb][r][dq] = vr[16 * dq];
+      }
+    // masks and the tile max of query qi
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * kb + 4 * g + r;
+        const bool vis = key < Lk && (!kp || !kp[key]) && (!causal || key <= qi);
+        st[kb][r] = vis ? st[kb][r] : -INFINITY;
+        tmax = fmaxf(tmax, st[kb][r]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = mn == -INFINITY ? 1.f : expf(m - mn);
+    float ts = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = st[kb][r] == -INFINITY ? 0.f : expf(st[kb][r] - mn);
+        st[kb][r] = p;
+        ts += p;
+      }
+    ts += __shfl_xor(ts, 16, 64);
+    ts += __shfl_xor(ts, 32, 64);
+    l = l * alpha + ts;
+    m = mn;
+    // O rows are queries 4 g + r': their factors from lanes c16 = 4 g + r'
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+      for (int dq = 0; dq < 4; ++dq) oacc[dq][r] *= ar;
+    }
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dq = 0; dq < 4; ++dq)
+          oacc[dq] = __builtin_amdgcn_mfma_f32_16x16x4f32(st[kb][r], vf[kb][r][dq], oacc[dq], 0, 0, 0);
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qr = q0 + 4 * g + r;
+    const float ir = __shfl(inv, 4 * g + r, 64);
+    if (qr < Lq) {
+      float* orow = o + (long)(b * Lq + qr) * ldo + h * D + c16;
+#pragma unroll
+      for (int dq = 0; dq < 4; ++dq) orow[16 * dq] = oacc[dq][r] * ir;
+    }
+  }
+  if (g == 0 && qi < Lq) lse[(long)bh * Lq + qi] = l > 0.f ? m + logf(l) : INFINITY;
+}
+
 // P / dS materialisation: ws_p = dropped P, ws_s = dS  ([B*H, Lq, Lk])
 __global__ void attn_bwd_ps_f32(int B, int H, int Lq, int Lk, int D, const float* q, long ldq,
                                 const float* k, long ldk, const float* v, long ldv,
@@ -1581,6 +1709,12 @@ extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_
   return SMER_OK;
 }
 
+// SMER_ATTN_F32_MFMA=0 keeps the fp32 forward on attn_fwd_f32 (A/B, tests)
+static bool smer_attn_f32_mfma() {
+  const char* e = getenv("SMER_ATTN_F32_MFMA");
+  return !(e && e[0] == '0');
+}
+
 static int attn_fwd_impl(int dtype, int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
                          const void* k, long ldk, const void* v, long ldv, void* o, long ldo,
                          float* lse, const uint8_t* kpm, int causal, float scale, float drop_p,
@@ -1604,6 +1738,13 @@ static int attn_fwd_impl(int dtype, int B, int H, int Lq, int Lk, int D, const v
     else if (D == 128) fwd_bf16_launch<128>(B, H, Lq, Lk, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal, scale, thr, seed, ds, (uint64_t*)drop_mask, drop_mask_in, q8, s);
     else return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_attn_fwd(bf16): head dim must be 32, 64 or 128");
   } else if (dtype == SMER_F32) {
+    if (D == 64 && thr == 0 && al16(q) && al16(k) && ldq % 4 == 0 && ldk % 4 == 0 && smer_attn_f32_mfma()) {
+      dim3 grid((Lq + 63) / 64, B * H);
+      hipLaunchKernelGGL(attn_fwd_f32_mfma, grid, dim3(256), 0, s, B, H, Lq, Lk, (const float*)q, ldq,
+                         (const float*)k, ldk, (const float*)v, ldv, (float*)o, ldo, lse, kpm, causal, scale);
+      SMER_CHECK_LAUNCH("smer_attn_fwd");
+      return SMER_OK;
+    }
     SMER_REQUIRE((size_t)Lk * 16 <= 160 * 1024, "smer_attn_fwd(f32): Lk too large");
     dim3 grid((Lq + 3) / 4, B * H);
     hipLaunchKernelGGL(attn_fwd_f32, grid, dim3(256), (size_t)Lk * 16, s, B, H, Lq, Lk, D,

@@ -2316,6 +2316,88 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_f32_kernel(int M, int
   }
 }
 
+// fp32 NT GEMM on the fp32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products and
+// sums): the parity-mode prefill (encoder Linears and the cross K/V of a
+// ~1k-token source: 104 us per Linear on the VALU tile kernel) and fp32
+// training forwards.  64x64 tiles, 4 waves of 32x32 (2x2 MFMA blocks); the
+// contraction of a 64-deep chunk runs in lane-group order (MFMA c sums
+// k = 16 g + c over the lane groups g), so a lane streams 16 consecutive
+// floats of one A row and one B row per block straight from global memory
+// (the 4 waves share rows through L1), next chunk requested before this
+// chunk's 64 MFMAs.
+__global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(int M, int N, int K, const float* __restrict__ A,
+                                                            long lda, const float* __restrict__ B, long ldb,
+                                                            GemmEpi e) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.y * 64 + (wave >> 1) * 32, n0 = blockIdx.x * 64 + (wave & 1) * 32;
+  const float* ap[2];
+  const float* bp[2];
+  bool aok[2], bok[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = m0 + 16 * i + c16, c = n0 + 16 * i + c16;
+    aok[i] = r < M;
+    bok[i] = c < N;
+    ap[i] = A + (long)(aok[i] ? r : 0) * lda + 16 * g;
+    bp[i] = B + (long)(bok[i] ? c : 0) * ldb + 16 * g;
+  }
+  auto load = [&](int k0, float4 (&fa)[2][4], float4 (&fb)[2][4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int k = k0 + 16 * g + 4 * t;
+        const bool kok = k < K;  // K % 4 == 0: a float4 is all in or all out
+        fa[i][t] = (aok[i] && kok) ? *reinterpret_cast<const float4*>(ap[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
+        fb[i][t] = (bok[i] && kok) ? *reinterpret_cast<const float4*>(bp[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
+      }
+  };
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 fa[2][4], fb[2][4];
+  load(0, fa, fb);
+  for (int k0 = 0; k0 < K; k0 += 64) {
+    float4 na[2][4], nb[2][4];
+    if (k0 + 64 < K) load(k0 + 64, na, nb);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float a = q == 0 ? fa[i][t].x : q == 1 ? fa[i][t].y : q == 2 ? fa[i][t].z : fa[i][t].w;
+            const float b = q == 0 ? fb[j][t].x : q == 1 ? fb[j][t].y : q == 2 ? fb[j][t].z : fb[j][t].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+          }
+    if (k0 + 64 < K) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { fa[i][t] = na[i][t]; fb[i][t] = nb[i][t]; }
+    }
+  }
+  // D[row 4g + r][col c16] of each block
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        epi_apply<float>(e, M, N, m0 + 16 * i + 4 * g + r, n0 + 16 * j + c16, acc[i][j][r]);
+}
+
+// SMER_GEMM_F32_MFMA=0 keeps fp32 NT shapes on the VALU tile kernel (A/B, tests)
+static bool smer_gemm_f32_mfma() {
+  const char* e = getenv("SMER_GEMM_F32_MFMA");
+  return !(e && e[0] == '0');
+}
+
 template <bool AK, bool BKC>
 static void launch_f32(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                        const GemmEpi& e, hipStream_t s) {
@@ -2327,6 +2409,12 @@ static void launch_f32(int M, int N, int K, const void* A, long lda, const void*
     return;
   }
   dim3 grid((N + 63) / 64, (M + 63) / 64);
+  if (AK && BKC && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+      (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && smer_gemm_f32_mfma()) {
+    hipLaunchKernelGGL(gemm_f32_mfma_kernel, grid, dim3(256), 0, s, M, N, K, (const float*)A, lda,
+                       (const float*)B, ldb, e);
+    return;
+  }
   hipLaunchKernelGGL((gemm_f32_kernel<AK, BKC>), grid, dim3(256), 0, s, M, N, K,
                      (const float*)A, lda, (const float*)B, ldb, e);
 }
@@ -2567,6 +2655,165 @@ extern "C" int smer_linear_decode(int M, int N, int K, const void* A, long lda, 
   e.vec = a16(bias, 8) && a16(residual, ldr) && a16(C, ldc) && a16(Cf, ldcf);
   launch_bf16<true, true>(M, N, K, A, lda, W, ldw, e, nullptr, 0, (hipStream_t)stream);
   SMER_CHECK_LAUNCH("smer_linear_decode");
+  return SMER_OK;
+}
+
+// fp32 decode Linear with the post-norm LayerNorm in its prologue (the
+// parity-mode decode step: LN3 -> next QKV, LN1 -> cross Q, LN2 -> FFN1,
+// final norm -> vocab head), gemm_skinny_f32_kernel's 4-column workgroups.
+// The weights of the (single, K <= 2048) load round are requested first, so
+// their HBM latency overlaps the row statistics; each workgroup normalises
+// its rows into LDS with ln_row_stats / ln_apply (the fp32 LayerNorm
+// kernel's arithmetic: same bits), workgroup 0 also stores them to X.
+__global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, int N, int K,
+                                                                         const float* __restrict__ Y, long ldy,
+                                                                         const float* __restrict__ gamma,
+                                                                         const float* __restrict__ beta, float eps,
+                                                                         float* __restrict__ X, long ldx,
+                                                                         const float* __restrict__ B, long ldb,
+                                                                         GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char xs_raw[];
+  float* xs = reinterpret_cast<float*>(xs_raw);  // mrows x K
+  __shared__ float red[SKF_NW][SKF_BM][SKF_BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = lane >> 4, kq = lane & 15;
+  const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
+  const int col = n0 + cq;
+  const bool colok = col < N;
+  const int mrows = min(SKF_BM, M - m0);
+  const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  float4 b[SKF_UNR];
+#pragma unroll
+  for (int u = 0; u < SKF_UNR; ++u) {
+    const int k = (wave + u * SKF_NW) * 64;
+    b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
+  }
+  const int nch = K >> 3;
+  for (int rr = wave; rr < mrows; rr += SKF_NW) {  // wave-uniform
+    const int row = m0 + rr;
+    float v[LNR_MAXC][8], mu, rs;
+    ln_row_stats<float>(Y + (long)row * ldy, K, eps, lane, v, mu, rs);
+#pragma unroll
+    for (int c = 0; c < LNR_MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nch) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gamma[ch * 8 + i], beta[ch * 8 + i]);
+        float* dst = xs + rr * K + ch * 8;
+        *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        if (X && blockIdx.x == 0) {
+          float* xo = X + (long)row * ldx + ch * 8;
+          *reinterpret_cast<float4*>(xo) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(xo + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float acc[SKF_BM];
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < SKF_UNR; ++u) {
+    const int k = (wave + u * SKF_NW) * 64 + 4 * kq;
+    if (k >= K) continue;
+#pragma unroll
+    for (int r = 0; r < SKF_BM; ++r) {
+      if (r < mrows) {
+        const float4 a = *reinterpret_cast<const float4*>(xs + r * K + k);
+        acc[r] = fmaf(a.x, b[u].x, acc[r]);
+        acc[r] = fmaf(a.y, b[u].y, acc[r]);
+        acc[r] = fmaf(a.z, b[u].z, acc[r]);
+        acc[r] = fmaf(a.w, b[u].w, acc[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) {
+    if (r < mrows) {
+      acc[r] += __shfl_xor(acc[r], 1, 64);
+      acc[r] += __shfl_xor(acc[r], 2, 64);
+      acc[r] += __shfl_xor(acc[r], 4, 64);
+      acc[r] += __shfl_xor(acc[r], 8, 64);
+    }
+  }
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < SKF_BM; ++r) red[wave][r][cq] = acc[r];
+  }
+  __syncthreads();
+  if (tid < SKF_BM * SKF_BN) {
+    const int r = tid / SKF_BN, c = tid % SKF_BN;
+    if (r < mrows && n0 + c < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < SKF_NW; ++w) t += red[w][r][c];
+      epi_apply<float>(e, M, N, m0 + r, n0 + c, t);
+    }
+  }
+}
+
+static GemmEpi decode_epi(const float* bias, int relu, const void* residual, long ldr, void* C, long ldc,
+                          float* Cf, long ldcf, void* kv, long kv_row_stride, long kv_req_stride,
+                          const int32_t* kv_req, const int32_t* kv_pos, int kv_col0) {
+  GemmEpi e{};
+  e.bias = bias; e.alpha = 1.f; e.relu = relu; e.residual = residual; e.ldr = ldr;
+  e.drop_scale = 1.f; e.C = C; e.ldc = ldc; e.Cf = Cf; e.ldcf = ldcf;
+  e.kv = kv; e.kv_row_stride = kv_row_stride; e.kv_req_stride = kv_req_stride;
+  e.kv_req = kv_req; e.kv_pos = kv_pos; e.kv_col0 = kv_col0;
+  return e;
+}
+
+// fp32 smer_linear_decode (parity-mode decode step): every operand fp32
+extern "C" int smer_linear_decode_f32(int M, int N, int K, const void* A, long lda, const void* W,
+                                      long ldw, const float* bias, int relu, const void* residual,
+                                      long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
+                                      long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
+                                      const int32_t* kv_pos, int kv_col0, smer_stream_t stream) {
+  SMER_REQUIRE(M > 0 && M <= 64 && N > 0 && K > 0, "smer_linear_decode_f32: sizes (M <= 64)");
+  SMER_REQUIRE(A && W && (C || Cf), "smer_linear_decode_f32: null operand");
+  SMER_REQUIRE(K % 4 == 0 && lda % 4 == 0 && ldw % 4 == 0 && aligned16(A) && aligned16(W),
+               "smer_linear_decode_f32: K / strides / alignment");
+  SMER_REQUIRE(!kv || (kv_req && kv_pos && kv_col0 >= 0 && kv_col0 < N), "smer_linear_decode_f32: kv scatter arguments");
+  const GemmEpi e = decode_epi(bias, relu, residual, ldr, C, ldc, Cf, ldcf, kv, kv_row_stride, kv_req_stride,
+                               kv_req, kv_pos, kv_col0);
+  const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+  hipLaunchKernelGGL(gemm_skinny_f32_kernel, grid, dim3(64 * SKF_NW), 0, (hipStream_t)stream, M, N, K,
+                     (const float*)A, lda, (const float*)W, ldw, e);
+  SMER_CHECK_LAUNCH("smer_linear_decode_f32");
+  return SMER_OK;
+}
+
+// fp32 smer_linear_decode_ln
+extern "C" int smer_linear_decode_ln_f32(int M, int N, int K, const void* Y, long ldy, const float* gamma,
+                                         const float* beta, float eps, void* X, long ldx, const void* W,
+                                         long ldw, const float* bias, int relu, const void* residual,
+                                         long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
+                                         long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
+                                         const int32_t* kv_pos, int kv_col0, smer_stream_t stream) {
+  SMER_REQUIRE(M > 0 && M <= 64 && N > 0 && K > 0, "smer_linear_decode_ln_f32: sizes (M <= 64)");
+  SMER_REQUIRE(K % 8 == 0 && K <= SKF_NW * SKF_UNR * 64 && K <= 64 * 8 * LNR_MAXC,
+               "smer_linear_decode_ln_f32: K % 8 == 0 and K <= 2048");
+  SMER_REQUIRE(Y && W && gamma && beta && (C || Cf), "smer_linear_decode_ln_f32: null operand");
+  SMER_REQUIRE(ldy % 4 == 0 && ldw % 4 == 0 && aligned16(Y) && aligned16(W) &&
+                   (!X || (aligned16(X) && ldx % 4 == 0)),
+               "smer_linear_decode_ln_f32: strides / alignment");
+  SMER_REQUIRE(!kv || (kv_req && kv_pos && kv_col0 >= 0 && kv_col0 < N), "smer_linear_decode_ln_f32: kv scatter arguments");
+  const GemmEpi e = decode_epi(bias, relu, residual, ldr, C, ldc, Cf, ldcf, kv, kv_row_stride, kv_req_stride,
+                               kv_req, kv_pos, kv_col0);
+  const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+  const size_t lds = (size_t)std::min(M, SKF_BM) * K * sizeof(float);
+  static bool attr_set = false;  // up to 128 KiB of dynamic LDS (16 rows x 2048)
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_skinny_ln_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        SKF_BM * 2048 * (int)sizeof(float));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(gemm_skinny_ln_f32_kernel, grid, dim3(64 * SKF_NW), lds, (hipStream_t)stream, M, N, K,
+                     (const float*)Y, ldy, gamma, beta, eps, (float*)X, ldx, (const float*)W, ldw, e);
+  SMER_CHECK_LAUNCH("smer_linear_decode_ln_f32");
   return SMER_OK;
 }
 

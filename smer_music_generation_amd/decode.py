@@ -154,6 +154,11 @@ class DecodeSession:
         scale = 1.0 / math.sqrt(D)
         sstride = self.Tmax * 2 * d
         cstride = 2 * H * self.Smax * D
+        if dt == torch.float32 and M <= 64 and os.environ.get("SMER_DECODE_F32_FUSED", "1") == "1":
+            if self.logits_t is None:
+                self.logits_t = torch.empty(M, eng.V, device=dev)
+            self._run_fused_layers_f32(x, scale, sstride, cstride)
+            return
         fused = dt == torch.bfloat16
         if fused:
             if self.logits_t is None:
@@ -270,6 +275,45 @@ class DecodeSession:
         x, _, _ = eng._ln(y_prev, n_prev, dt)  # last LN3; the final norm feeds the head below
         ops.linear_decode_ln(x, W.dec_norm[0], W.dec_norm[1], W.fc_w, W.fc_b,
                              out_f32=self.logits_t[r0:r1])
+
+    def _run_fused_layers_f32(self, x, scale, sstride, cstride):
+        """fp32 (parity-mode) decoder step, 8 launches per layer instead of 12:
+        the post-norm LayerNorms run in the prologue of the Linear that
+        consumes them (ops.linear_decode_ln: LN3 -> next QKV, LN1 -> cross Q,
+        LN2 -> FFN1, final norm -> vocab head; the LN output also stored as
+        the next residual, the LayerNorm kernel's bits) and the QKV epilogue
+        appends the new K/V to the cache (no kv_scatter launch).  Every
+        operand fp32; the attention and the plain Linears as in _run."""
+        eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
+        H, D, M = eng.H, eng.D, self.M
+        pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
+        y_prev = n_prev = None
+        for li, L in enumerate(W.dec):
+            cache = self.self_kv[li]
+            kv = dict(kv=cache, kv_req=req_t, kv_pos=pos_t, kv_row_stride=2 * d,
+                      kv_req_stride=sstride, kv_col0=d)
+            if y_prev is None:  # layer 0: x is the embedding (no norm in front)
+                qkv = ops.linear_decode(x, L.sa_w, L.sa_b, **kv)
+            else:
+                x = torch.empty(M, d, dtype=dt, device=dev)
+                qkv = ops.linear_decode_ln(y_prev, n_prev[0], n_prev[1], L.sa_w, L.sa_b, x_out=x, **kv)
+            o = torch.empty(M, d, dtype=dt, device=dev)
+            ops.attn_decode(qkv[:, :d], cache, cache.view(-1)[d:], req_t, nks_t, o, H=H, D=D,
+                            row_stride=2 * d, req_stride=sstride, scale=scale)
+            y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=x)
+            x1 = torch.empty(M, d, dtype=dt, device=dev)
+            qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
+            cc = self.cross_kv[li]
+            oc = torch.empty(M, d, dtype=dt, device=dev)
+            ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
+                            row_stride=D, req_stride=cstride, head_stride=self.Smax * D, scale=scale)
+            y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
+            x2 = torch.empty(M, d, dtype=dt, device=dev)
+            h = ops.linear_decode_ln(y2, L.n2[0], L.n2[1], L.l1_w, L.l1_b, relu=True, x_out=x2)
+            y_prev = ops.linear(h, L.l2_w, L.l2_b, residual=x2)
+            n_prev = L.n3
+        x, _, _ = eng._ln(y_prev, n_prev, dt)  # last LN3; the final norm feeds the head below
+        ops.linear_decode_ln(x, W.dec_norm[0], W.dec_norm[1], W.fc_w, W.fc_b, out_f32=self.logits_t)
 
     def _ensure_graph(self):
         if self.graph is not None or not self.use_graph:

@@ -300,14 +300,15 @@ def kv_scatter(src, cache, row_req, row_pos, *, row_stride, req_stride):
 
 def linear_decode(x, w, bias=None, *, relu=False, residual=None, out=None, out_f32=None, kv=None,
                   kv_req=None, kv_pos=None, kv_row_stride=0, kv_req_stride=0, kv_col0=0):
-    """Decode-step Linear (bf16, M <= 256): out = x @ w^T + bias (+relu)
-    (+residual); output columns >= kv_col0 are also appended to the K/V
-    cache `kv` at (kv_req[m], kv_pos[m])."""
+    """Decode-step Linear (bf16, M <= 256; fp32, M <= 64): out = x @ w^T +
+    bias (+relu) (+residual); output columns >= kv_col0 are also appended to
+    the K/V cache `kv` at (kv_req[m], kv_pos[m])."""
     M, K = x.shape
     N = w.shape[0]
     if out is None and out_f32 is None:
         out = torch.empty(M, N, device=x.device, dtype=x.dtype)
-    call("smer_linear_decode", M, N, K, _p(x), _ld(x), _p(w), _ld(w), _p(bias), int(bool(relu)),
+    fn = "smer_linear_decode_f32" if x.dtype == torch.float32 else "smer_linear_decode"
+    call(fn, M, N, K, _p(x), _ld(x), _p(w), _ld(w), _p(bias), int(bool(relu)),
          _p(residual), _ld(residual) if residual is not None else 0, _p(out),
          _ld(out) if out is not None else 0, _p(out_f32), _ld(out_f32) if out_f32 is not None else 0,
          _p(kv), int(kv_row_stride), int(kv_req_stride), _p(kv_req), _p(kv_pos), int(kv_col0),
@@ -324,7 +325,8 @@ def linear_decode_ln(y, gamma, beta, w, bias=None, *, x_out=None, eps=1e-5, relu
     N = w.shape[0]
     if out is None and out_f32 is None:
         out = torch.empty(M, N, device=y.device, dtype=y.dtype)
-    call("smer_linear_decode_ln", M, N, K, _p(y), _ld(y), _p(gamma), _p(beta), float(eps), _p(x_out),
+    fn = "smer_linear_decode_ln_f32" if y.dtype == torch.float32 else "smer_linear_decode_ln"
+    call(fn, M, N, K, _p(y), _ld(y), _p(gamma), _p(beta), float(eps), _p(x_out),
          _ld(x_out) if x_out is not None else 0, _p(w), _ld(w), _p(bias), int(bool(relu)),
          _p(residual), _ld(residual) if residual is not None else 0, _p(out),
          _ld(out) if out is not None else 0, _p(out_f32), _ld(out_f32) if out_f32 is not None else 0,

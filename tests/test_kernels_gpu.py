@@ -342,6 +342,42 @@ def test_attention_fwd_bwd(dtype, D, Lq, Lk, causal, pad):
     assert rel_err(dv, vf.grad) < tolb
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,causal", [(1, 8, 1100, 1100, False), (2, 3, 200, 333, False),
+                                              (2, 2, 130, 130, True), (3, 2, 17, 70, False)])
+def test_attention_f32_mfma_matches_wave_kernel(monkeypatch, B, H, Lq, Lk, causal):
+    """The fp32 flash forward on the fp32 MFMA (parity-mode prefill) against
+    the wave-per-query kernel and fp32 torch, incl. a fully padded sequence
+    (O = 0, lse = +inf) and ragged tiles."""
+    O = ops()
+    D = 64
+    q = torch.randn(B * Lq, H * D, device=dev) * 2
+    kv = torch.randn(B * Lk, 2 * H * D, device=dev)
+    k, v = kv[:, : H * D], kv[:, H * D:]
+    kpm = torch.zeros(B, Lk, device=dev, dtype=torch.uint8)
+    kpm[0, Lk - Lk // 4:] = 1
+    if B > 1:
+        kpm[-1] = 1  # a sequence with no visible key
+    scale = 1.0 / math.sqrt(D)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SMER_ATTN_F32_MFMA", flag)
+        o = torch.empty(B * Lq, H * D, device=dev)
+        lse = torch.empty(B, H, Lq, device=dev)
+        O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D, kpm=kpm, causal=causal, scale=scale)
+        torch.cuda.synchronize()
+        outs[flag] = (o, lse)
+    o, lse = outs["1"]
+    # reference on the sequences with visible keys
+    nb = B - 1 if B > 1 else B
+    ro, rlse = attn_ref(q[: nb * Lq], k[: nb * Lk], v[: nb * Lk], nb, H, Lq, Lk, D, kpm[:nb], causal, scale)
+    assert rel_err(o[: nb * Lq], ro) < 2e-5
+    assert (lse[:nb] - rlse).abs().max().item() < 1e-4
+    assert rel_err(o, outs["0"][0]) < 2e-5
+    if B > 1:
+        assert torch.all(o[nb * Lq:] == 0) and torch.all(torch.isinf(lse[nb:]))
+        assert torch.all(outs["0"][0][nb * Lq:] == 0)
+
+
 @pytest.mark.parametrize("D", [32, 64])
 def test_attention_padded_keys_with_huge_scores(D):
     """Padded keys whose raw scores dwarf the valid ones: they must not leak
@@ -869,6 +905,37 @@ def test_linear_decode_ln_is_layernorm_then_linear(M, N, K):
     assert torch.equal(got, ref)
     assert torch.equal(c2, c1)
     assert torch.equal(lf_got, lf_ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(2, 1536, 512), (2, 309, 512), (4, 2048, 512), (37, 512, 768),
+                                   (64, 264, 2048)])
+def test_linear_decode_f32_ln_and_kv(M, N, K):
+    """fp32 decode Linears (the parity-mode decode step): the LayerNorm
+    prologue stores the fp32 LayerNorm kernel's bits, the product matches
+    fp32 torch, the K/V append equals the output columns."""
+    O = ops()
+    y = torch.randn(M, K, device=dev) * 2 + 0.5
+    g, be = torch.randn(K, device=dev), torch.randn(K, device=dev)
+    w = torch.randn(N, K, device=dev) / math.sqrt(K)
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    xln = torch.empty_like(y)
+    O.layernorm(y, g, be, xln, torch.empty(M, device=dev), torch.empty(M, device=dev))
+    col0 = N // 3
+    R, T = 3, M // 3 + 1
+    cache = torch.zeros(R, T, N - col0, device=dev)
+    req = torch.arange(M, device=dev, dtype=torch.int32) % R
+    pos = torch.arange(M, device=dev, dtype=torch.int32) // R
+    x_out = torch.empty_like(y)
+    got = O.linear_decode_ln(y, g, be, w, b, relu=True, x_out=x_out, kv=cache, kv_req=req, kv_pos=pos,
+                             kv_row_stride=N - col0, kv_req_stride=T * (N - col0), kv_col0=col0)
+    lin = O.linear_decode(xln, w, b, residual=res)
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, xln)
+    ref = torch.relu(xln @ w.t() + b)
+    assert rel_err(got, ref) < 1e-5
+    assert torch.equal(cache[req.long(), pos.long()], got[:, col0:])
+    assert rel_err(lin, xln @ w.t() + b + res) < 1e-5
 
 
 @pytest.mark.parametrize("S,dm", [(300, 512), (2100, 512), (700, 768)])
