@@ -1933,6 +1933,11 @@ extern "C" int smer_attn_weights(int dtype, int B, int H, int Lq, int Lk, int D,
 }
 
 // SMER_DECODE_ODD_FIRST=0: blocks in plain row order (A/B)
+// SMER_DEC_PIPE_SMALL=0: grids of <= 128 blocks take the unpipelined form
+static bool smer_dec_pipe_small() {
+  const char* e = getenv("SMER_DEC_PIPE_SMALL");
+  return !(e && e[0] == '0');
+}
 static int smer_dec_odd_first() {
   const char* e = getenv("SMER_DECODE_ODD_FIRST");
   return (e && e[0] == '0') ? 0 : 1;
@@ -2006,7 +2011,11 @@ extern "C" int smer_attn_decode(int dtype, int n_rows, int H, int D, const void*
     // 4 steps of loads in flight per block, short self-attention caches 4 x 2
     const long cap_rows = head_stride != D ? head_stride / (row_stride > 0 ? row_stride : 1)
                                            : req_stride / (row_stride > 0 ? row_stride : 1);
-    const bool big = cap_rows >= 512, pipe = cap_rows >= 2048;
+    // pipelined loads also for few blocks (the batch-1 plugin step: 16
+    // blocks stream a ~1k-key memory each); the same arithmetic as the
+    // unpipelined 8-wave form, so the logits do not depend on the batch
+    const bool big = cap_rows >= 512;
+    const bool pipe = cap_rows >= 2048 || (big && (long)n_rows * H <= 128 && smer_dec_pipe_small());
     const int odd = smer_dec_odd_first();
 #define SMER_DEC_VEC(T, L)                                                                        \
   if (pipe)                                                                                       \
