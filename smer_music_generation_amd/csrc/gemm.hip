@@ -2016,6 +2016,17 @@ static bool smer_wgrad256s_enabled() {
   const char* e = getenv("SMER_WGRAD256S");
   return !(e && e[0] == '0');
 }
+// work items of the 256x256 weight-gradient grid (SMER_WGRAD256_SLOTS;
+// default one per CU): fewer split-K slices write fewer fp32 slab bytes and
+// leave CUs to the main stream's kernels (A/B runs)
+static long smer_wgrad256_slots() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD256_SLOTS");
+    v = e ? std::max(8, atoi(e)) : smer_num_cus();
+  }
+  return v;
+}
 static int smer_wgrad256_depth() {
   static int v = -1;
   if (v < 0) {
@@ -2163,7 +2174,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                          ((long)M * N) % 4 == 0;
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
     const long cus = smer_num_cus();
-    long ns = std::min<long>(cus / std::max<long>(1, t2), K / smer_wgrad256_depth());
+    long ns = std::min<long>(smer_wgrad256_slots() / std::max<long>(1, t2), K / smer_wgrad256_depth());
     ns = std::min<long>(ns, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
     ns = std::max<long>(1, std::min<long>(ns, 64));
     if (cf_only && t2 * ns * 4 >= 3 * cus) {
