@@ -1409,16 +1409,20 @@ struct DecQ {
 
 template <int D, int NT, int DM>
 __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int tid, float* qs,
-                                               bf16* xs) {
+                                               bf16* xs, bool need_q) {
   constexpr int TPO = NT / D;    // threads per query value
   constexpr int KT = DM / TPO;   // K per thread (multiple of 8)
   const int lane = tid & 63, wave = tid >> 6;
   const int d = tid / TPO, part = tid % TPO;
-  // the head's weight row slice, requested before the row statistics
+  // the head's weight row slice, requested before the row statistics (not
+  // at all for a row with <= 1 key: softmax over one key is 1 whatever q,
+  // e.g. a decode session's dummy rows)
   const bf16* wr = dq.wq + (long)(h * D + d) * dq.ldw + part * KT;
   bf16x8 wv[KT / 8];
+  if (need_q) {
 #pragma unroll
-  for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+    for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+  }
   if (wave == 0) {
     float v[LNR_MAXC][8], mu, rs;
     ln_row_stats<bf16>(dq.y + (long)r * dq.ldy, dq.dmodel, dq.eps, lane, v, mu, rs);
@@ -1436,19 +1440,26 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
     }
   }
   __syncthreads();
-  float acc = 0.f;
+  if (need_q) {  // block-uniform
+    float acc = 0.f;
 #pragma unroll
-  for (int j = 0; j < KT / 8; ++j) {
-    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + part * KT + 8 * j);
+    for (int j = 0; j < KT / 8; ++j) {
+      const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + part * KT + 8 * j);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc = fmaf((float)xv[i], (float)wv[j][i], acc);
+      for (int i = 0; i < 8; ++i) acc = fmaf((float)xv[i], (float)wv[j][i], acc);
+    }
+#pragma unroll
+    for (int w = 1; w < TPO; w <<= 1) acc += __shfl_xor(acc, w, 64);
+    if (part == 0) qs[d] = (float)(bf16)(acc + dq.bq[h * D + d]);
+  } else if (part == 0) {
+    qs[d] = 0.f;
   }
-#pragma unroll
-  for (int w = 1; w < TPO; w <<= 1) acc += __shfl_xor(acc, w, 64);
-  if (part == 0) qs[d] = (float)(bf16)(acc + dq.bq[h * D + d]);
   __syncthreads();
 }
 
+#ifndef SMER_DEC_QSKIP
+#define SMER_DEC_QSKIP 1  // tools/build_variant.sh ... -DSMER_DEC_QSKIP=0: the A/B baseline
+#endif
 template <typename T, int LPK, int UNR, int NW, bool PIPE = false, int QP = 0>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
@@ -1501,7 +1512,7 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     static_assert(sizeof(T) == 2, "the query prologue is bf16");
     __shared__ float qs[LPK * VEC];
     __shared__ __attribute__((aligned(16))) bf16 xs[QP];
-    dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs);
+    dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, SMER_DEC_QSKIP ? nk > 1 : true);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) qv[i] = qs[sub * VEC + i];
   } else {
