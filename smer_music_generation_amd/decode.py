@@ -87,6 +87,8 @@ class DecodeSession:
         self.logits_h = torch.zeros(M, eng.V, dtype=torch.float32).pin_memory()
         self.use_graph = use_graph
         self.graph = None
+        # step(): the row-table H2D and logits D2H copies inside the step graph
+        self._graph_copies = os.environ.get("SMER_DECODE_GRAPH_COPY", "1") == "1"
         self.logits_t = None
 
     def refresh_weights(self):
@@ -318,18 +320,30 @@ class DecodeSession:
     def _ensure_graph(self):
         if self.graph is not None or not self.use_graph:
             return
-        # warm up eagerly once (allocator, library load), then capture
+        # warm up eagerly once (allocator, library load), then capture; the
+        # step graph also holds the row-table H2D copies and the logits D2H
+        # copy (memcpy nodes: no separate copy launches per token)
         self._run()
         torch.cuda.synchronize()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        self.graph = _capture(s, self._run)
+        if self._graph_copies:
+            self.graph = _capture(s, self._run_with_copies)
+        else:
+            self.graph = _capture(s, self._run)
         torch.cuda.current_stream().wait_stream(s)
 
-    def _load_feeds(self, feeds):
+    def _run_with_copies(self):
+        self.ids_t.copy_(self.ids_h, non_blocking=True)
+        self.meta_t.copy_(self.meta_h, non_blocking=True)
+        self._run()
+        self.logits_h.copy_(self.logits_t, non_blocking=True)
+
+    def _load_feeds(self, feeds, copy=True):
         """Host-built step rows: feeds = [(slot, new_token_ids (1 or 2),
         first_position)]; every other row is a dummy into the trash slot.
-        Returns the rows of each feed's last token."""
+        Returns the rows of each feed's last token.  copy=False: the pinned
+        host rows only (the captured step graph copies them itself)."""
         Tm = self.Tmax
         ids = self.ids_h.numpy()
         meta = self.meta_h.numpy()
@@ -353,20 +367,27 @@ class DecodeSession:
                 meta[2, r0 + k] = p0 + k + 1
                 meta[3, r0 + k] = max(int(self.src_len[slot]), 1)
             last.append(2 * slot + 1)
-        self.ids_t.copy_(self.ids_h, non_blocking=True)
-        self.meta_t.copy_(self.meta_h, non_blocking=True)
+        if copy:
+            self.ids_t.copy_(self.ids_h, non_blocking=True)
+            self.meta_t.copy_(self.meta_h, non_blocking=True)
         return last
 
     def step(self, feeds):
         """feeds: list of (slot, new_token_ids (1 or 2), first_position).
         Returns fp32 logits [len(feeds), V] (numpy) of each feed's LAST new
         token.  Slots not fed this step are dummies."""
-        last = self._load_feeds(feeds)
         if self.use_graph:
+            # the first call's eager warm-up reads the device row tables
+            first = self.graph is None
+            last = self._load_feeds(feeds, copy=first or not self._graph_copies)
             self._ensure_graph()
             self.graph.replay()
-        else:
-            self._run()
+            if not self._graph_copies:
+                self.logits_h.copy_(self.logits_t, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return self.logits_h.numpy()[last]
+        last = self._load_feeds(feeds)
+        self._run()
         self.logits_h.copy_(self.logits_t, non_blocking=True)
         torch.cuda.current_stream().synchronize()
         return self.logits_h.numpy()[last]
