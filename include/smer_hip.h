@@ -232,6 +232,20 @@ int smer_linear_decode_ln_f32(int M, int N, int K, const void* Y, long ldy, cons
                               long ldr, void* C, long ldc, float* Cf, long ldcf, void* kv,
                               long kv_row_stride, long kv_req_stride, const int32_t* kv_req,
                               const int32_t* kv_pos, int kv_col0, smer_stream_t stream);
+/* Flash-decoding for the fp32 plugin step (transformer.py:463 per token):
+ * smer_attn_decode_split_f32 attends each (row, head) over 8 key slices in
+ * separate blocks, writing unnormalised partials {m, l, 0, 0, acc[64]}
+ * (68 floats) at part[((row * H + head) * 8 + slice) * 68];
+ * smer_linear_decode_merge_f32 merges them in fixed order into its input
+ * rows (K = 64 * H) and applies the Linear + bias (+ReLU) (+residual)
+ * (the cross-attention out-projection, transformer.py:463-464).  fp32, D 64. */
+int smer_attn_decode_split_f32(int n_rows, int H, int D, const void* q, long ldq, const void* kcache,
+                               const void* vcache, long row_stride, long req_stride, long head_stride,
+                               const int32_t* row_req, const int32_t* row_nkeys, float* part, float scale,
+                               smer_stream_t stream);
+int smer_linear_decode_merge_f32(int M, int N, int K, const float* part, const void* W, long ldw,
+                                 const float* bias, int relu, const void* residual, long ldr, void* C,
+                                 long ldc, float* Cf, long ldcf, smer_stream_t stream);
 /* One greedy grammar step for R requests (generation.py:528-687).
  * logits: fp32 [2R, >=V] rows (request r's last fed token at row 2r+1).
  * state: int32 [R, nst>=9] = pos, flags(sep|cont<<1|pitch<<2|rest<<3), span

@@ -63,6 +63,10 @@ SIGNATURES = {
     "smer_linear_decode_ln_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
                                           c_long, P, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
                                           c_long, P, P, c_int, P]),
+    "smer_attn_decode_split_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, c_long, P, P, P,
+                                           c_float, P]),
+    "smer_linear_decode_merge_f32": (c_int, [c_int, c_int, c_int, P, P, c_long, P, c_int, P, c_long, P, c_long, P,
+                                             c_long, P]),
     "smer_fp8_quantize_workspace": (c_size, []),
     "smer_fp8_quantize": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P]),
     "smer_fp8_quantize_segments": (c_int, [c_int, P, P, P, c_int, P]),

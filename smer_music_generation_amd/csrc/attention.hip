@@ -1460,12 +1460,16 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
 #ifndef SMER_DEC_QSKIP
 #define SMER_DEC_QSKIP 1  // tools/build_variant.sh ... -DSMER_DEC_QSKIP=0: the A/B baseline
 #endif
-template <typename T, int LPK, int UNR, int NW, bool PIPE = false, int QP = 0>
+// NS > 0: the keys of a (row, head) split over NS blocks (blockIdx.z), each
+// writing its unnormalised partial {m, l, pad, pad, acc[D]} (fp32, 4 + D
+// floats) to part[((row * H + head) * NS + z) * (4 + D)] instead of o (the
+// consumer merges them in fixed order: flash-decoding for few rows)
+template <typename T, int LPK, int UNR, int NW, bool PIPE = false, int QP = 0, int NS = 0>
 __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     const T* __restrict__ q, long ldq, const T* __restrict__ kc, const T* __restrict__ vc,
     long row_stride, long req_stride, long head_stride, const int32_t* __restrict__ row_req,
     const int32_t* __restrict__ row_nkeys, T* __restrict__ o, long ldo, float scale,
-    DecQ dq = DecQ{}, int odd_first = 0) {
+    DecQ dq = DecQ{}, int odd_first = 0, float* __restrict__ part = nullptr) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int GPW = 64 / LPK;  // key groups per wave
   constexpr int KPB = NW * GPW;  // keys per block step
@@ -1480,7 +1484,14 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   const int h = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int sub = lane % LPK, grp = wave * GPW + lane / LPK;
-  const int nk = row_nkeys[r];
+  const int nk_all = row_nkeys[r];
+  // this block's keys [kb, nk): all of them, or split NS's slice
+  int kb = 0, nk = nk_all;
+  if constexpr (NS > 0) {
+    const int chunk = ((nk_all + NS - 1) / NS + KPB - 1) / KPB * KPB;
+    kb = min(nk_all, (int)blockIdx.z * chunk);
+    nk = min(nk_all, kb + chunk);
+  }
   const long base = (long)row_req[r] * req_stride + h * head_stride + sub * VEC;
   float qv[VEC];
   float m = -INFINITY, l = 0.f, acc[VEC];
@@ -1523,8 +1534,8 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   // (QP: requesting the first key step's K / V before the query prologue
   // measured slower, 368 vs 336 us per decode step, and at C5's 4096-key
   // memories 46.4k vs 47.5k tokens/s: issued after it)
-  if (PIPE && nk > 0) load_step(0, kr, vr);
-  for (int j0 = 0; j0 < nk; j0 += KPB * UNR) {
+  if (PIPE && nk > kb) load_step(kb, kr, vr);
+  for (int j0 = kb; j0 < nk; j0 += KPB * UNR) {
     uint4 kn[UNR], vn[UNR];
     if constexpr (PIPE) {
       if (j0 + KPB * UNR < nk) load_step(j0 + KPB * UNR, kn, vn);
@@ -1600,6 +1611,13 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
       ll += red_l[w][tid] * c;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) out[i] += red_a[w][tid][i] * c;
+    }
+    if constexpr (NS > 0) {
+      float* pr = part + (((long)r * gridDim.x + h) * NS + blockIdx.z) * (4 + LPK * VEC);
+      if (tid == 0) { pr[0] = mm; pr[1] = ll; }
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) pr[4 + tid * VEC + i] = out[i];
+      return;
     }
     const float inv = ll > 0.f ? 1.f / ll : 0.f;
     T* op = o + (long)r * ldo + h * (LPK * VEC) + tid * VEC;
@@ -1952,6 +1970,30 @@ static bool smer_dec_pipe_small() {
 static int smer_dec_odd_first() {
   const char* e = getenv("SMER_DECODE_ODD_FIRST");
   return (e && e[0] == '0') ? 0 : 1;
+}
+
+// fp32 decode attention over NS = 8 key slices per (row, head): partial
+// {m, l, acc} records for smer_linear_decode_merge_f32 (the plugin's batch-1
+// step: 16 blocks of the unsplit form stream a ~1k-key memory each)
+extern "C" int smer_attn_decode_split_f32(int n_rows, int H, int D, const void* q, long ldq, const void* kcache,
+                                          const void* vcache, long row_stride, long req_stride, long head_stride,
+                                          const int32_t* row_req, const int32_t* row_nkeys, float* part,
+                                          float scale, smer_stream_t stream) {
+  SMER_REQUIRE(D == 64 && H > 0, "smer_attn_decode_split_f32: head dim 64");
+  SMER_REQUIRE(q && kcache && vcache && row_req && row_nkeys && part, "smer_attn_decode_split_f32: null pointer");
+  auto al = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  SMER_REQUIRE(al(q) && al(kcache) && al(vcache) && al(part) && ldq % 4 == 0 && row_stride % 4 == 0 &&
+                   req_stride % 4 == 0 && (head_stride <= 0 || head_stride % 4 == 0),
+               "smer_attn_decode_split_f32: alignment / strides");
+  if (n_rows == 0) return SMER_OK;
+  if (head_stride <= 0) head_stride = D;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(H, n_rows, 8);
+  hipLaunchKernelGGL((attn_decode_vec_kernel<float, 16, 2, 4, false, 0, 8>), grid, dim3(256), 0, s, (const float*)q,
+                     ldq, (const float*)kcache, (const float*)vcache, row_stride, req_stride, head_stride, row_req,
+                     row_nkeys, (float*)nullptr, 0L, scale, DecQ{}, 0, part);
+  SMER_CHECK_LAUNCH("smer_attn_decode_split_f32");
+  return SMER_OK;
 }
 
 extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, long ldy,

@@ -2766,6 +2766,95 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, 
   }
 }
 
+// fp32 decode Linear whose input rows are the attention output merged from
+// smer_attn_decode_split_f32's per-slice partials (the cross-attention
+// out-projection of the plugin's fp32 step): the prologue merges the NS = 8
+// {m, l, acc} records of each (row, head) in fixed order into LDS rows
+// (o = sum_s e^(m_s - m) acc_s / sum_s e^(m_s - m) l_s), then the GEMM of
+// gemm_skinny_ln_f32_kernel.  The weights of the single load round are
+// requested first.
+constexpr int DEC_NS = 8;
+__global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_merge_f32_kernel(int M, int N, int K,
+                                                                            const float* __restrict__ part,
+                                                                            const float* __restrict__ B, long ldb,
+                                                                            GemmEpi e) {
+  extern __shared__ __attribute__((aligned(16))) char xs_raw[];
+  float* xs = reinterpret_cast<float*>(xs_raw);  // mrows x K
+  __shared__ float red[SKF_NW][SKF_BM][SKF_BN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = lane >> 4, kq = lane & 15;
+  const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
+  const int col = n0 + cq;
+  const bool colok = col < N;
+  const int mrows = min(SKF_BM, M - m0);
+  const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  float4 b[SKF_UNR];
+#pragma unroll
+  for (int u = 0; u < SKF_UNR; ++u) {
+    const int k = (wave + u * SKF_NW) * 64;
+    b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
+  }
+  const int H = K / 64;
+  for (int t = wave; t < mrows * H; t += SKF_NW) {  // wave-uniform: (row, head) records
+    const int rr = t / H, hh = t % H;
+    const float* pr = part + ((long)(m0 + rr) * H + hh) * DEC_NS * 68;
+    float ms = -INFINITY;
+#pragma unroll
+    for (int z = 0; z < DEC_NS; ++z) ms = fmaxf(ms, pr[z * 68]);
+    float L = 0.f, o = 0.f;
+#pragma unroll
+    for (int z = 0; z < DEC_NS; ++z) {
+      const float mz = pr[z * 68];
+      const float w = mz == -INFINITY ? 0.f : __expf(mz - ms);
+      L += pr[z * 68 + 1] * w;
+      o += pr[z * 68 + 4 + lane] * w;
+    }
+    xs[rr * K + hh * 64 + lane] = o * (L > 0.f ? 1.f / L : 0.f);
+  }
+  __syncthreads();
+  float acc[SKF_BM];
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int u = 0; u < SKF_UNR; ++u) {
+    const int k = (wave + u * SKF_NW) * 64 + 4 * kq;
+    if (k >= K) continue;
+#pragma unroll
+    for (int r = 0; r < SKF_BM; ++r) {
+      if (r < mrows) {
+        const float4 a = *reinterpret_cast<const float4*>(xs + r * K + k);
+        acc[r] = fmaf(a.x, b[u].x, acc[r]);
+        acc[r] = fmaf(a.y, b[u].y, acc[r]);
+        acc[r] = fmaf(a.z, b[u].z, acc[r]);
+        acc[r] = fmaf(a.w, b[u].w, acc[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < SKF_BM; ++r) {
+    if (r < mrows) {
+      acc[r] += __shfl_xor(acc[r], 1, 64);
+      acc[r] += __shfl_xor(acc[r], 2, 64);
+      acc[r] += __shfl_xor(acc[r], 4, 64);
+      acc[r] += __shfl_xor(acc[r], 8, 64);
+    }
+  }
+  if (kq == 0) {
+#pragma unroll
+    for (int r = 0; r < SKF_BM; ++r) red[wave][r][cq] = acc[r];
+  }
+  __syncthreads();
+  if (tid < SKF_BM * SKF_BN) {
+    const int r = tid / SKF_BN, c = tid % SKF_BN;
+    if (r < mrows && n0 + c < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < SKF_NW; ++w) t += red[w][r][c];
+      epi_apply<float>(e, M, N, m0 + r, n0 + c, t);
+    }
+  }
+}
+
 static GemmEpi decode_epi(const float* bias, int relu, const void* residual, long ldr, void* C, long ldc,
                           float* Cf, long ldcf, void* kv, long kv_row_stride, long kv_req_stride,
                           const int32_t* kv_req, const int32_t* kv_pos, int kv_col0) {
@@ -2825,6 +2914,29 @@ extern "C" int smer_linear_decode_ln_f32(int M, int N, int K, const void* Y, lon
   hipLaunchKernelGGL(gemm_skinny_ln_f32_kernel, grid, dim3(64 * SKF_NW), lds, (hipStream_t)stream, M, N, K,
                      (const float*)Y, ldy, gamma, beta, eps, (float*)X, ldx, (const float*)W, ldw, e);
   SMER_CHECK_LAUNCH("smer_linear_decode_ln_f32");
+  return SMER_OK;
+}
+
+// fp32 decode Linear on the merged split-attention partials (see above)
+extern "C" int smer_linear_decode_merge_f32(int M, int N, int K, const float* part, const void* W, long ldw,
+                                            const float* bias, int relu, const void* residual, long ldr, void* C,
+                                            long ldc, float* Cf, long ldcf, smer_stream_t stream) {
+  SMER_REQUIRE(M > 0 && M <= 64 && N > 0 && K > 0 && K % 64 == 0 && K <= SKF_NW * SKF_UNR * 64,
+               "smer_linear_decode_merge_f32: sizes (M <= 64, K = 64 * heads <= 2048)");
+  SMER_REQUIRE(part && W && (C || Cf) && ldw % 4 == 0 && aligned16(W),
+               "smer_linear_decode_merge_f32: operands / alignment");
+  const GemmEpi e = decode_epi(bias, relu, residual, ldr, C, ldc, Cf, ldcf, nullptr, 0, 0, nullptr, nullptr, 0);
+  const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+  const size_t lds = (size_t)std::min(M, SKF_BM) * K * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_skinny_merge_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        SKF_BM * 2048 * (int)sizeof(float));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(gemm_skinny_merge_f32_kernel, grid, dim3(64 * SKF_NW), lds, (hipStream_t)stream, M, N, K, part,
+                     (const float*)W, ldw, e);
+  SMER_CHECK_LAUNCH("smer_linear_decode_merge_f32");
   return SMER_OK;
 }
 

@@ -289,6 +289,10 @@ class DecodeSession:
         eng, W, dt, dev, d = self.eng, self.W, self.dt, self.dev, self.d
         H, D, M = eng.H, eng.D, self.M
         pos_t, req_t, nks_t, nkc_t = self.meta_t[0], self.meta_t[1], self.meta_t[2], self.meta_t[3]
+        # cross attention as flash-decoding (8 key slices per (row, head),
+        # merged in the out-projection's prologue): the unsplit form runs
+        # 2 * R * H blocks, 16 at batch 1
+        self._split_f32 = D == 64 and d <= 2048 and os.environ.get("SMER_DECODE_SPLIT_F32", "1") == "1"
         y_prev = n_prev = None
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
@@ -306,10 +310,17 @@ class DecodeSession:
             x1 = torch.empty(M, d, dtype=dt, device=dev)
             qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
             cc = self.cross_kv[li]
-            oc = torch.empty(M, d, dtype=dt, device=dev)
-            ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
-                            row_stride=D, req_stride=cstride, head_stride=self.Smax * D, scale=scale)
-            y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
+            if self._split_f32:  # 8 key slices per (row, head), merged by the out-projection
+                part = torch.empty(M, H, ops.DEC_SPLITS, 68, device=dev)
+                ops.attn_decode_split_f32(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, part, H=H,
+                                          D=D, row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
+                                          scale=scale)
+                y2 = ops.linear_decode_merge_f32(part, L.ca_ow, L.ca_ob, M=M, residual=x1)
+            else:
+                oc = torch.empty(M, d, dtype=dt, device=dev)
+                ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
+                                row_stride=D, req_stride=cstride, head_stride=self.Smax * D, scale=scale)
+                y2 = ops.linear(oc, L.ca_ow, L.ca_ob, residual=x1)
             x2 = torch.empty(M, d, dtype=dt, device=dev)
             h = ops.linear_decode_ln(y2, L.n2[0], L.n2[1], L.l1_w, L.l1_b, relu=True, x_out=x2)
             y_prev = ops.linear(h, L.l2_w, L.l2_b, residual=x2)

@@ -284,6 +284,29 @@ def attn_decode_qln(y, gamma, beta, wq, bq, kcache, vcache, row_req, row_nkeys, 
          _p(row_nkeys), _p(out), _ld(out), float(scale), _stream())
 
 
+DEC_SPLITS = 8  # key slices of attn_decode_split_f32 (csrc DEC_NS)
+
+
+def attn_decode_split_f32(q, kcache, vcache, row_req, row_nkeys, part, *, H, D, row_stride, req_stride,
+                          scale, head_stride=0):
+    """fp32 decode attention over 8 key slices per (row, head): partial
+    records part [rows, H, 8, 68] (see smer_hip.h)."""
+    call("smer_attn_decode_split_f32", q.shape[0], H, D, _p(q), _ld(q), _p(kcache), _p(vcache),
+         int(row_stride), int(req_stride), int(head_stride), _p(row_req), _p(row_nkeys), _p(part),
+         float(scale), _stream())
+
+
+def linear_decode_merge_f32(part, w, bias=None, *, M, residual=None, relu=False, out=None):
+    """out = merge(part) @ w^T + bias (+relu) (+residual), fp32; merge()
+    combines attn_decode_split_f32's slices into the attention output rows."""
+    N, K = w.shape
+    if out is None:
+        out = torch.empty(M, N, device=w.device, dtype=torch.float32)
+    call("smer_linear_decode_merge_f32", M, N, K, _p(part), _p(w), _ld(w), _p(bias), int(bool(relu)),
+         _p(residual), _ld(residual) if residual is not None else 0, _p(out), _ld(out), None, 0, _stream())
+    return out
+
+
 def kv_scatter_heads(src, cache, row_req, row_pos, *, H, D, req_stride, kv_stride, head_stride):
     """Rows of [K heads | V heads] into a head-major cache (see smer_hip.h)."""
     if src.shape[1] != 2 * H * D:

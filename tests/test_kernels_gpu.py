@@ -970,6 +970,30 @@ def test_attn_decode_qln_is_ln_linear_attention(S, dm):
     assert rel_err(got, ref) < 2e-2, rel_err(got, ref)
 
 
+@pytest.mark.parametrize("S,M", [(1100, 2), (300, 6), (40, 2), (2500, 4)])
+def test_attn_decode_split_f32_merge(S, M):
+    """fp32 flash-decoding (8 key slices per (row, head), partials merged in
+    the out-projection's prologue) == smer_attn_decode then the Linear
+    (+bias, +residual), incl. rows with 1 key and slices with no key."""
+    O = ops()
+    H, D, dm, R = 8, 64, 512, 3
+    cache = torch.randn(R, 2, H, S, D, device=dev)
+    q = torch.randn(M, dm, device=dev)
+    req = torch.arange(M, device=dev, dtype=torch.int32) % R
+    nk = torch.tensor([S, 1, S // 3, 5, S - 1, 2][:M], device=dev, dtype=torch.int32)
+    kw = dict(H=H, D=D, row_stride=D, req_stride=2 * H * S * D, head_stride=S * D, scale=0.125)
+    o = torch.empty(M, dm, device=dev)
+    O.attn_decode(q, cache, cache.view(-1)[H * S * D:], req, nk, o, **kw)
+    w = torch.randn(dm, dm, device=dev) / math.sqrt(dm)
+    b, res = torch.randn(dm, device=dev), torch.randn(M, dm, device=dev)
+    ref = O.linear(o, w, b, residual=res)
+    part = torch.empty(M, H, O.DEC_SPLITS, 68, device=dev)
+    O.attn_decode_split_f32(q, cache, cache.view(-1)[H * S * D:], req, nk, part, **kw)
+    got = O.linear_decode_merge_f32(part, w, b, M=M, residual=res)
+    torch.cuda.synchronize()
+    assert rel_err(got, ref) < 1e-5, rel_err(got, ref)
+
+
 # ------------------------------------------------------------ fp8
 def _e4m3_ref(x, amax):
     """e4m3 bytes of x * (448 / amax): f32 scale by IEEE division, f32
