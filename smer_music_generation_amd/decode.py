@@ -303,6 +303,8 @@ class DecodeSession:
             else:
                 x = torch.empty(M, d, dtype=dt, device=dev)
                 qkv = ops.linear_decode_ln(y_prev, n_prev[0], n_prev[1], L.sa_w, L.sa_b, x_out=x, **kv)
+            # (the self attention stays unsplit: its <= ~400-key caches
+            # measured 0.306 vs 0.296 ms per step split)
             o = torch.empty(M, d, dtype=dt, device=dev)
             ops.attn_decode(qkv[:, :d], cache, cache.view(-1)[d:], req_t, nks_t, o, H=H, D=D,
                             row_stride=2 * d, req_stride=sstride, scale=scale)
