@@ -3353,11 +3353,339 @@ extern "C" int smer_fp8_quantize(int rows, int cols, const void* x, long ldx, vo
   return SMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// fp8 (e4m3) staggered 256x256 GEMM for long-K NT products (the C4 fp8
+// dgrads, K >= 1024): gemm256s_bf16_kernel's schedule, slots and epilogue
+// with the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 scales,
+// 2x the bf16 rate): a 32-deep bf16 k-step of the LDS image is 64 e4m3 per
+// row, exactly one K = 64 MFMA step; a wave's 128x64 outputs are 4 x 2
+// blocks of 32 x 32 (8 MFMAs of 64 cycles per k-step, as the bf16 kernel's
+// 32 of 16).  Lane l holds A[row l & 31][k 32 (l >> 5) .. + 31] (32 B: two
+// 16-B chunks, contiguous under the chunk ^ 2 bit2(row) swizzle).
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma_f8_32(i32x8 a, i32x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+__device__ __forceinline__ i32x8 f8_cat(uint4 lo, uint4 hi) {
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+template <int OFF>
+__device__ __forceinline__ uint4 lds_u4_off(uint32_t a) {
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+// the 6 fragments of one k-step (12 reads): A blocks i (rows wm*128 + 32 i),
+// B blocks q (columns wn*64 + 32 q)
+__device__ __forceinline__ void gs_frags_f8(uint32_t slot_lds, int wm, int wn, int lane, i32x8 (&af)[4],
+                                            i32x8 (&bfr)[2]) {
+  const int r32 = lane & 31, h = lane >> 5;
+  const uint32_t off = r32 * 64 + (((2 * h) ^ gs_swz(r32)) << 4);
+  const uint32_t ab = slot_lds + wm * 8192 + off;
+  const uint32_t bb = slot_lds + GS_OP + wn * 4096 + off;
+  bfr[0] = f8_cat(lds_u4_off<0>(bb), lds_u4_off<16>(bb));
+  bfr[1] = f8_cat(lds_u4_off<2048>(bb), lds_u4_off<2064>(bb));
+  af[0] = f8_cat(lds_u4_off<0>(ab), lds_u4_off<16>(ab));
+  af[1] = f8_cat(lds_u4_off<2048>(ab), lds_u4_off<2064>(ab));
+  af[2] = f8_cat(lds_u4_off<4096>(ab), lds_u4_off<4112>(ab));
+  af[3] = f8_cat(lds_u4_off<6144>(ab), lds_u4_off<6160>(ab));
+}
+// fp32 staging index for the 32x32 C layout (lanes l and l + 32 write rows 4
+// apart: column bit 5 flipped on rows with bit 2 set)
+__device__ __forceinline__ int gs_ep_idx32(int row, int col) { return row * 256 + (col ^ (((row >> 2) & 1) << 5)); }
+__device__ __forceinline__ void f8_retire(i32x8 (&a)[4], i32x8 (&b)[2]) {
+  lds_wait<0>();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int i = 0; i < 2; ++i) asm volatile("" : "+v"(b[i]));
+}
+
+__global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int K,
+                                                              const uint8_t* __restrict__ A8, long lda8,
+                                                              const uint8_t* __restrict__ B8, long ldb8,
+                                                              const float* __restrict__ a_inv,
+                                                              const float* __restrict__ b_inv, GemmEpi e) {
+  constexpr bool BKC = true;
+  // the LDS-DMA moves bytes: address the e4m3 rows as bf16 pairs, so a
+  // 32-"element" k-step is 64 fp8 and every slot / piece is the bf16 kernel's
+  const bf16* A = reinterpret_cast<const bf16*>(A8);
+  const bf16* B = reinterpret_cast<const bf16*>(B8);
+  const long lda = lda8 / 2, ldb = ldb8 / 2;
+  e.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3, lw = wave & 3;
+  const bool loader = wm == 1;  // waves 4-7: every DMA; waves 0-3: every store
+  const int nbm = M / G2, nbn = N / G2;
+  const int nwg = nbm * nbn;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  const int nk = K / (2 * GS_KS);  // 64 fp8 per k-step; host: nk >= 4
+  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);
+  const long ldx = e.residual ? e.ldr : e.ldg;
+  const uint32_t lds0 = lds_u32(smem);
+  const int g = lane >> 4, c16 = lane & 15;
+  constexpr int EP_LD = G2 + 4;
+
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // e.dbg: tiles 0 and 1, 4 stamps each
+  int tcount = 0;
+  for (int jj = braw >> 3; jj < xcount; jj += pstride, ++tcount) {
+    const int wgid = xstart + jj;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int m0 = (first_m + within % gsz) * G2, n0 = (within / gsz) * G2;
+    const bool stamp = e.dbg != nullptr && tcount < 2;
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[0] = t_; else st[4] = t_; }
+
+    f32x16 acc[4][2];  // 32x32 blocks: rows wm*128 + 32 i, columns wn*64 + 32 q
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // operand bases of this tile; k-step k adds k * 32 columns (A, NT B) or
+    // k * 32 rows (NN B)
+    const bf16* At = A + (long)m0 * lda;
+    const bf16* Bt = BKC ? B + (long)n0 * ldb : B + n0;
+    const long bstep = BKC ? GS_KS : (long)GS_KS * ldb;
+
+    // prologue: k-steps 0..2 in flight, k-step 0 landed before the first
+    // barrier (after the first tile, k-steps 0 and 1 were issued during the
+    // previous tile's epilogue)
+    if (loader) {
+      if (tcount == 0) {
+        gs_issue<BKC>(lds0 + 0 * GS_SLOT, At, lda, Bt, ldb, lw, lane);
+        gs_issue<BKC>(lds0 + 1 * GS_SLOT, At + GS_KS, lda, Bt + bstep, ldb, lw, lane);
+      }
+      gs_issue<BKC>(lds0 + 2 * GS_SLOT, At + 2 * GS_KS, lda, Bt + 2 * bstep, ldb, lw, lane);
+      vm_wait<16>();
+    }
+    gs_bar();
+    if (loader) gs_bar();  // the lagging half: one barrier behind from here
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[1] = t_; else st[5] = t_; }
+
+    for (int j = 0; j < nk; ++j) {
+      // R(j): fragment reads of slot j & 3; a loader issues the B half of
+      // k-step j+3 (into the slot k-step j-1 left: every wave retired its
+      // reads of it before its previous M phase) and waits for k-step j+1.
+      // Issue order per loader: B(t) in R(t-3), A(t) in M(t-3).
+      i32x8 bfr[2], af[4];
+      gs_frags_f8(lds0 + (j & 3) * GS_SLOT, wm, wn, lane, af, bfr);
+      const bool do_k = loader && j + 3 < nk;
+      const uint32_t kslot = lds0 + ((j + 3) & 3) * GS_SLOT;
+      const bf16* Aj = At + (long)(j + 3) * GS_KS;
+      const bf16* Bj = Bt + (j + 3) * bstep;
+      if (do_k) {
+#pragma unroll
+        for (int t = 4; t < 8; ++t) gs_piece<BKC>(t, kslot, Aj, lda, Bj, ldb, lw, lane);
+      }
+      if (loader) {
+        if (j + 3 < nk) {
+          vm_wait<12>();  // k-step j+1 landed (B, A of j+2 and B of j+3 fly)
+        } else if (j + 3 == nk) {
+          vm_wait<8>();
+        } else if (j + 2 == nk) {  // k-step nk-1 landed; bias / X(0) may fly on
+          if (xsrc && e.bias) vm_wait<5>();
+          else if (xsrc) vm_wait<4>();
+          else if (e.bias) vm_wait<1>();
+          else vm_wait<0>();
+        }
+      }
+      gs_bar();
+      // M(j): 32 MFMAs; a loader slips the A half of k-step j+3 in behind
+      // every 8 of them (an LDS-DMA piece costs ~60-185 issue cycles: all
+      // eight in one phase stretched it past the partner's 32 MFMAs)
+      f8_retire(af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[i][q] = mfma_f8_32(af[i], bfr[q], acc[i][q]);
+        if (do_k) {  // one A piece of k-step j+3 behind every 2 MFMAs (64 cycles each)
+          __builtin_amdgcn_sched_barrier(0);
+          gs_piece<BKC>(i, kslot, Aj, lda, Bj, ldb, lw, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (loader && j + 3 == nk) {
+        // the epilogue's bias row and first X rows, beyond the four slots
+        // (the bias through LDS: a register load would be a vmcnt wait
+        // hipcc places itself, on the storers' outstanding stores)
+        if (e.bias) gs_bias_load(lds0 + GS_BIAS, e.bias + n0, lane);
+        if (xsrc) gs_xload(lds0 + GS_XA, xsrc + (long)m0 * ldx + n0, ldx, lw, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      gs_bar();
+    }
+    if (!loader) gs_bar();  // realign the halves
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[2] = t_; else st[6] = t_; }
+
+    // ---- epilogue: eight 32-row passes through fp32 LDS staging ---------
+    // The owning half (rows 128 wm .. +127) stages its accumulators; all 512
+    // threads apply bias / ReLU / dropout / residual or gate to 2 items of 8
+    // columns; the storers store theirs, the loaders hand theirs to the
+    // storers as bf16 through OUT (stored one pass later): loaders never
+    // store, so their vmcnt holds DMAs only.  The loaders first issue the
+    // next tile's k-steps 0 and 1 (slots 0-1), which land under this
+    // epilogue, then stream X one pass ahead.
+    const int jn = jj + pstride;
+    const bool has_next = jn < xcount;
+    if (loader && has_next) {
+      const int wn2 = xstart + jn;
+      const int grp2 = wn2 / (GM * nbn);
+      const int gsz2 = min(nbm - grp2 * GM, GM);
+      const int win2 = wn2 % (GM * nbn);
+      const int m1 = (grp2 * GM + win2 % gsz2) * G2, n1 = (win2 / gsz2) * G2;
+      const bf16* At1 = A + (long)m1 * lda;
+      const bf16* Bt1 = BKC ? B + (long)n1 * ldb : B + n1;
+      if (xsrc)  // X(1) ahead of them: its wait then passes over them
+        gs_xload(lds0 + GS_XB, xsrc + (long)(m0 + GS_EPR) * ldx + n0, ldx, lw, lane);
+      gs_issue<BKC>(lds0 + 0 * GS_SLOT, At1, lda, Bt1, ldb, lw, lane);
+      gs_issue<BKC>(lds0 + 1 * GS_SLOT, At1 + GS_KS, lda, Bt1 + bstep, ldb, lw, lane);
+    } else if (loader && xsrc) {
+      gs_xload(lds0 + GS_XB, xsrc + (long)(m0 + GS_EPR) * ldx + n0, ldx, lw, lane);
+    }
+    float* ep = reinterpret_cast<float*>(smem + GS_EP);
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int ch = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      if (loader) {  // X(pass) (and at pass 0 the bias) landed
+        if (xsrc) {
+          if (pass >= 1 && pass < 7)  // X(pass+1) into the slot X(pass-1) left
+            gs_xload(lds0 + (((pass + 1) & 1) ? GS_XB : GS_XA),
+                     xsrc + (long)(m0 + GS_EPR * (pass + 1)) * ldx + n0, ldx, lw, lane);
+          if (pass <= 1) {
+            if (has_next) vm_wait<20>();
+            else vm_wait<4>();
+          } else if (pass < 7) {
+            vm_wait<4>();
+          } else {
+            vm_wait<0>();
+          }
+        } else if (pass == 0 && e.bias) {
+          if (has_next) vm_wait<16>();
+          else vm_wait<0>();
+        }
+      }
+      if (wm == (pass >> 2)) {  // 32x32 row block i = pass & 3: row (r&3) + 8 (r>>2) + 4 (lane>>5)
+        const int i = pass & 3;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ep[gs_ep_idx32((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), wn * 64 + q * 32 + (lane & 31))] = acc[i][q][r];
+      }
+      smer_lds_barrier();  // staging rows written, X(pass) and the bias landed
+      if (pass == 0 && e.bias) {
+        const float* bl = reinterpret_cast<const float*>(smem + GS_BIAS) + ch * 8;
+        const float4 b0 = *reinterpret_cast<const float4*>(bl);
+        const float4 b1 = *reinterpret_cast<const float4*>(bl + 4);
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      }
+      // storers: the loaders' items of the previous pass (bf16 in OUT)
+      if (!loader && pass >= 1) {
+        const char* ob = smem + GS_OUT + ((pass - 1) & 1) * 8192;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int lr = (tid >> 5) + 8 * c;  // 0..15 -> pass rows 8..15, 24..31
+          const int row = (lr & 7) + 8 + 16 * (lr >> 3);
+          const bf16x8 o = *reinterpret_cast<const bf16x8*>(ob + lr * 512 + ch * 16);
+          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)(m0 + (pass - 1) * GS_EPR + row) * e.ldc + n0 + ch * 8) = o;
+        }
+      }
+      const char* xs = smem + ((pass & 1) ? GS_XB : GS_XA);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int row = (tid >> 5) + 16 * c;  // storers rows 0..7, 16..23; loaders 8..15, 24..31
+        const int grow = m0 + pass * GS_EPR + row, gcol = n0 + ch * 8;
+        float v[8];
+        const float4 a = *reinterpret_cast<const float4*>(ep + gs_ep_idx32(row, ch * 8));
+        const float4 b = *reinterpret_cast<const float4*>(ep + gs_ep_idx32(row, ch * 8) + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = v[k] * e.alpha + bv[k];
+        if (e.relu) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+        }
+        if (e.drop_thr)
+          smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
+        if (xsrc) {
+          const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
+          if (e.residual) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += (float)xv[k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (float)xv[k] > 0.f ? v[k] * e.gate_scale : 0.f;
+          }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
+        if (!loader) {
+          *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+        } else {
+          const int lr = (row & 7) + 8 * (row >> 4);
+          *reinterpret_cast<bf16x8*>(smem + GS_OUT + (pass & 1) * 8192 + lr * 512 + ch * 16) = o;
+        }
+      }
+      smer_lds_barrier();  // staging, X(pass) and OUT(pass - 1) read before they are rewritten
+    }
+    if (!loader) {  // the loaders' items of the last pass
+      const char* ob = smem + GS_OUT + 8192;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int lr = (tid >> 5) + 8 * c;
+        const int row = (lr & 7) + 8 + 16 * (lr >> 3);
+        const bf16x8 o = *reinterpret_cast<const bf16x8*>(ob + lr * 512 + ch * 16);
+        *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)(m0 + 7 * GS_EPR + row) * e.ldc + n0 + ch * 8) = o;
+      }
+    }
+    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[3] = t_; else st[7] = t_; }
+  }
+  if (e.dbg && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e.dbg[((long)blockIdx.x * 8 + wave) * 8 + k] = st[k];
+  }
+}
+
+
 extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                                const float* a_inv, const float* b_inv, const float* bias, int relu,
                                const void* residual, long ldr, float drop_p, uint32_t drop_seed,
                                void* C, long ldc, void* q8, long ldq8, const float* q8_scale,
                                unsigned* q8_amax, smer_stream_t stream);
+
+// The staggered fp8 kernel for whole-tile bf16-output products: opt-in
+// (SMER_GEMM256S_FP8=1 / 0 forces it on / off, read per call).  Isolated
+// and warm (tools/gemm256s_fp8_ab.py, C4 rows 65536, operands re-used across
+// iterations) it wins at K >= 1024 (FFN2 forward 122.3 vs 133.1 us, FFN1 /
+// QKV dgrads 113.8 / 125.1 vs 123.0 / 131.7) and loses at K = 768 (QKV
+// forward 160.7 vs 151.7); inside the C4 fp8 train step, whose operands
+// arrive cold from HBM, the same K >= 1024 calls ran slower (paired
+// kernel trace: 133.5 vs 129.3 us at the 130-us shapes, 794 vs 698 at the
+// vocabulary-long K) and the step did not move (86.3 vs 85.9 ms), so the
+// two-stage kernel stays the default.
+static bool smer_gemm256s_fp8_enabled(int K) {
+  (void)K;
+  const char* e = getenv("SMER_GEMM256S_FP8");
+  return e && e[0] == '1';
+}
 
 extern "C" int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                              const float* a_inv, const float* b_inv, const float* bias, int relu,
@@ -3403,6 +3731,19 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
     e.q8 = (uint8_t*)q8; e.ldq8 = ldq8; e.q8_scale = q8_scale; e.q8_amax = q8_amax;
   }
   hipStream_t s = (hipStream_t)stream;
+  const long tiles = (long)(M / G2) * (N / G2);
+  const int grid = tiles > smer_num_cus() ? (smer_num_cus() & ~7) : (int)tiles;
+  if (e.vec && !q8 && K % (2 * GS_KS) == 0 && K / (2 * GS_KS) >= 4 && smer_gemm256s_fp8_enabled(K)) {
+    static bool attr_s = false;
+    if (!attr_s) {
+      hipFuncSetAttribute((const void*)gemm256s_fp8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+      attr_s = true;
+    }
+    hipLaunchKernelGGL(gemm256s_fp8_kernel, dim3(grid), dim3(512), G2_LDS, s, M, N, K, (const uint8_t*)A, lda,
+                       (const uint8_t*)B, ldb, a_inv, b_inv, e);
+    SMER_CHECK_LAUNCH("smer_gemm_fp8");
+    return SMER_OK;
+  }
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)gemm256_fp8_kernel<false, false>,
@@ -3413,8 +3754,6 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
                         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * G2_STAGE);
     attr_set = true;
   }
-  const long tiles = (long)(M / G2) * (N / G2);
-  const int grid = tiles > smer_num_cus() ? (smer_num_cus() & ~7) : (int)tiles;
   if (!e.vec)  // (q8 requires e.vec)
     hipLaunchKernelGGL((gemm256_fp8_kernel<false, false>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N,
                        K, (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);

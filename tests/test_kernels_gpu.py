@@ -1022,6 +1022,51 @@ def test_gemm_fp8_exact_integer_layout():
     assert torch.equal(C.float().cpu(), ref.to(torch.bfloat16).float())
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 768, 1280), (4608, 4096, 256), (256, 256, 3072)])
+def test_gemm256s_fp8_matches_two_stage_kernel(monkeypatch, M, N, K):
+    """The staggered fp8 kernel (32x32x64 block-scaled MFMA) against the
+    two-stage 16x16x128 one on exact small-integer e4m3 operands: the fp32
+    accumulators are exact in both, so every epilogue (scale, bias, ReLU,
+    dropout, residual, ReLU gate) must agree bit for bit, and the plain
+    product must equal A.B^T.  (4608, 4096) is 288 tiles: the persistent
+    path with the next tile's k-steps issued under the epilogue; K = 256 is
+    the 4-k-step minimum."""
+    O = ops()
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    A = torch.randint(-4, 5, (M, K), generator=g).float()
+    B = torch.randint(-3, 4, (N, K), generator=g).float()
+    B[:, 0] += torch.arange(N) % 5
+    a8 = A.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    b8 = B.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    ai = torch.tensor([0.0123], device=dev)
+    bi = torch.tensor([0.37], device=dev)
+    one = torch.ones(1, device=dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    gate = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+
+    def run(flag):
+        monkeypatch.setenv("SMER_GEMM256S_FP8", flag)
+        outs = []
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        assert O.gemm_fp8(a8, one, b8, one, C)
+        outs.append(C)
+        C = torch.empty_like(C)
+        assert O.gemm_fp8(a8, ai, b8, bi, C, bias=bias, relu=True, residual=res, drop_p=0.1, seed=7)
+        outs.append(C)
+        C = torch.empty_like(C)
+        assert O.gemm_fp8_ex(a8, ai, b8, bi, C, gate=gate, gate_scale=1.25)
+        outs.append(C)
+        torch.cuda.synchronize()
+        return [c.cpu() for c in outs]
+
+    new, old = run("1"), run("0")
+    ref = (A.to(torch.float8_e4m3fn).float() @ B.to(torch.float8_e4m3fn).float().t()).to(torch.bfloat16)
+    assert torch.equal(new[0], ref)
+    for a, b in zip(new, old):
+        assert torch.equal(a, b)
+
+
 def test_fp8_quantize_and_gemm():
     """Per-tensor quantisation (amax + scaled e4m3 cast, matching torch's
     float8_e4m3fn rounding) and the scaled fp8 GEMM with the full epilogue
