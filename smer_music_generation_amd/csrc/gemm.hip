@@ -1959,14 +1959,11 @@ static bool smer_gemm256s_enabled(bool bkc, int N, int K) {
   return K >= 1024 || (!bkc && N >= 1024);
 }
 
-// SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests)
+// SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests;
+// read per call)
 static bool smer_gemm64_enabled() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SMER_GEMM64");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v == 1;
+  const char* e = getenv("SMER_GEMM64");
+  return !(e && e[0] == '0');
 }
 
 static int smer_num_cus() {
