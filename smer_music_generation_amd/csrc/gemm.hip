@@ -3431,7 +3431,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
   const int g = lane >> 4, c16 = lane & 15;
   constexpr int EP_LD = G2 + 4;
 
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // e.dbg: tiles 0 and 1, 4 stamps each
   int tcount = 0;
   for (int jj = braw >> 3; jj < xcount; jj += pstride, ++tcount) {
     const int wgid = xstart + jj;
@@ -3440,8 +3439,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
     const int gsz = min(nbm - first_m, GM);
     const int within = wgid % (GM * nbn);
     const int m0 = (first_m + within % gsz) * G2, n0 = (within / gsz) * G2;
-    const bool stamp = e.dbg != nullptr && tcount < 2;
-    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[0] = t_; else st[4] = t_; }
 
     f32x16 acc[4][2];  // 32x32 blocks: rows wm*128 + 32 i, columns wn*64 + 32 q
 #pragma unroll
@@ -3450,8 +3447,8 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // operand bases of this tile; k-step k adds k * 32 columns (A, NT B) or
-    // k * 32 rows (NN B)
+    // operand bases of this tile (bf16-pair units); k-step k adds k * 32
+    // pairs = 64 e4m3 columns
     const bf16* At = A + (long)m0 * lda;
     const bf16* Bt = BKC ? B + (long)n0 * ldb : B + n0;
     const long bstep = BKC ? GS_KS : (long)GS_KS * ldb;
@@ -3469,7 +3466,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
     }
     gs_bar();
     if (loader) gs_bar();  // the lagging half: one barrier behind from here
-    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[1] = t_; else st[5] = t_; }
 
     for (int j = 0; j < nk; ++j) {
       // R(j): fragment reads of slot j & 3; a loader issues the B half of
@@ -3499,9 +3495,8 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
         }
       }
       gs_bar();
-      // M(j): 32 MFMAs; a loader slips the A half of k-step j+3 in behind
-      // every 8 of them (an LDS-DMA piece costs ~60-185 issue cycles: all
-      // eight in one phase stretched it past the partner's 32 MFMAs)
+      // M(j): 8 MFMAs of 64 cycles; a loader slips one A piece of k-step
+      // j+3 in behind every 2 of them
       f8_retire(af, bfr);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
@@ -3527,7 +3522,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
       gs_bar();
     }
     if (!loader) gs_bar();  // realign the halves
-    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[2] = t_; else st[6] = t_; }
 
     // ---- epilogue: eight 32-row passes through fp32 LDS staging ---------
     // The owning half (rows 128 wm .. +127) stages its accumulators; all 512
@@ -3653,11 +3647,6 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
         *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)(m0 + 7 * GS_EPR + row) * e.ldc + n0 + ch * 8) = o;
       }
     }
-    if (stamp) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); if (tcount == 0) st[3] = t_; else st[7] = t_; }
-  }
-  if (e.dbg && lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e.dbg[((long)blockIdx.x * 8 + wave) * 8 + k] = st[k];
   }
 }
 
