@@ -1857,11 +1857,32 @@ __global__ void splitk_reduce_kernel(int M, int N, int ksplit, const float* __re
     return;
   }
   float4 a = *reinterpret_cast<const float4*>(slabs + idx);
-  for (int s = 1; s < ksplit; ++s) {
+  int s = 1;
+  for (; s + 4 <= ksplit; s += 4) {  // four slices' loads in flight, summed in slice order
+    float4 b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[u] = *reinterpret_cast<const float4*>(slabs + (long)(s + u) * MN + idx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w;
+    }
+  }
+  for (; s < ksplit; ++s) {
     float4 b = *reinterpret_cast<const float4*>(slabs + (long)s * MN + idx);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
   float v[4] = {a.x * alpha, a.y * alpha, a.z * alpha, a.w * alpha};
+  if ((N & 3) == 0 && (ldcf & 3) == 0 && (((uintptr_t)Cf) & 15) == 0) {  // the 4 items share a row
+    const long row = idx / N;
+    float* p = Cf + row * ldcf + (idx - row * N);
+    float4 o = make_float4(v[0], v[1], v[2], v[3]);
+    if (accumulate) {
+      const float4 c = *reinterpret_cast<const float4*>(p);
+      o.x = c.x + o.x; o.y = c.y + o.y; o.z = c.z + o.z; o.w = c.w + o.w;
+    }
+    *reinterpret_cast<float4*>(p) = o;
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     long e = idx + t;
