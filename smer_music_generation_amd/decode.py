@@ -90,6 +90,19 @@ class DecodeSession:
         # step(): the row-table H2D and logits D2H copies inside the step graph
         self._graph_copies = os.environ.get("SMER_DECODE_GRAPH_COPY", "1") == "1"
         self.logits_t = None
+        # the positional table the captured graphs address (pos_enc.extend()
+        # by a later session reallocates it: _pe_guard drops stale graphs)
+        self._pe_ptr = model.pos_enc.pe.data_ptr()
+
+    def _pe_guard(self):
+        """Drop the captured step / greedy graphs when the model's
+        positional table moved since they were captured (another session's
+        pos_enc.extend() freed the buffer they read)."""
+        ptr = self.model.pos_enc.pe.data_ptr()
+        if ptr != self._pe_ptr:
+            self.graph = None
+            self._greedy = None
+            self._pe_ptr = ptr
 
     def refresh_weights(self):
         self.W = self.eng.weights(self.dt)
@@ -156,7 +169,10 @@ class DecodeSession:
         scale = 1.0 / math.sqrt(D)
         sstride = self.Tmax * 2 * d
         cstride = 2 * H * self.Smax * D
-        if dt == torch.float32 and M <= 64 and os.environ.get("SMER_DECODE_F32_FUSED", "1") == "1":
+        # the fused fp32 layers need the LayerNorm-prologue Linear's limits
+        # (K = d_model a multiple of 8, at most 2048); other widths unfused
+        if (dt == torch.float32 and M <= 64 and d % 8 == 0 and d <= 2048
+                and os.environ.get("SMER_DECODE_F32_FUSED", "1") == "1"):
             if self.logits_t is None:
                 self.logits_t = torch.empty(M, eng.V, device=dev)
             self._run_fused_layers_f32(x, scale, sstride, cstride)
@@ -389,6 +405,7 @@ class DecodeSession:
         """feeds: list of (slot, new_token_ids (1 or 2), first_position).
         Returns fp32 logits [len(feeds), V] (numpy) of each feed's LAST new
         token.  Slots not fed this step are dummies."""
+        self._pe_guard()
         if self.use_graph:
             # the first call's eager warm-up reads the device row tables
             first = self.graph is None
@@ -459,6 +476,7 @@ class DecodeSession:
         R = len(spans)
         if R > self.R:
             raise ValueError("more spans than session slots")
+        self._pe_guard()
         dev = self.dev
         nm = max(1, max(s.n_masks for s in spans))
         cap = self.Tmax

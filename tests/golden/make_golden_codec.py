@@ -12,9 +12,13 @@ container on inputs that need no MIDI library:
   (velocity -1) and notes shorter than a grid step;
 * `note_to_event_name` (`encode.py:939-944`);
 * `bar_notes_to_event` (`encode.py:957-1141`) on bars whose notes end
-  inside the bar (no cross-bar continuation: that branch builds
-  `pretty_midi.Note` objects, and pretty_midi is absent here), with
-  continued notes from the previous bar as inputs.
+  inside the bar, with continued notes from the previous bar as inputs;
+* `bar_notes_to_event`'s cross-bar continuation branch
+  (`encode.py:1028-1040,1109-1121`): notes running past the bar line.  That
+  branch builds `pretty_midi.Note(pitch=, start=, end=, velocity=)` objects
+  (pretty_midi is absent here), so the empty stub module gets a recorder
+  class `Note` holding exactly those four attributes; the carried notes are
+  recorded as [pitch, start, end, velocity].
 
 RUN ONLY IN THE BUILD CONTAINER (imports /root/reference; the absent MIDI /
 music libraries are stubbed as EMPTY modules, as in make_golden_wire.py).
@@ -36,6 +40,18 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REF)
 for _m in ("pretty_midi", "music21", "coloredlogs", "tension_calculation"):
     sys.modules.setdefault(_m, types.ModuleType(_m))
+
+
+
+class _RecNote:
+    """Recorder standing for pretty_midi.Note on the continuation branch:
+    the four keyword attributes the reference passes and later reads."""
+
+    def __init__(self, pitch, start, end, velocity):
+        self.pitch, self.start, self.end, self.velocity = pitch, start, end, velocity
+
+
+sys.modules["pretty_midi"].Note = _RecNote
 
 import encode as ref_encode  # noqa: E402  (reference)
 
@@ -171,11 +187,57 @@ def bar_event_cases(rng):
     return recs
 
 
+def _cross_notes(rng, bar, n, step):
+    """Notes of one bar of which some run past the bar line (ties), chords
+    of tied and untied notes, and a continued note from the previous bar."""
+    notes = []
+    if rng.random() < 0.5:  # continued from the previous bar, maybe tied on
+        end = step * int(rng.integers(1, 8)) if rng.random() < 0.5 else bar + step * int(rng.integers(1, 12))
+        notes.append([int(rng.integers(40, 80)), 0.0, float(end), -1])
+    for _ in range(n):
+        start = rng.random() * (bar - 2 * step)
+        if rng.random() < 0.45:  # past the bar line
+            end = bar + step * rng.choice([0.5, 1, 3, 8, 17])
+        else:
+            end = min(start + step * rng.choice([0.3, 1, 2, 4, 8]), bar - step)
+            if end <= start:
+                end = start + 0.4 * step
+        notes.append([int(rng.integers(40, 80)), float(start), float(end), int(rng.integers(30, 120))])
+    if notes and rng.random() < 0.7:  # a chord on the last note, some members tied
+        p, s0, e0, v = notes[-1]
+        notes.append([p + 3, s0, e0 if rng.random() < 0.5 else bar + 2 * step, v])
+        notes.append([p + 7, s0 + step / 30, e0, v])
+    if notes and rng.random() < 0.3:  # a duplicate pitch in a chord
+        notes.append(list(notes[-1]))
+    return notes
+
+
+def cross_bar_cases(rng):
+    recs = []
+    for sig in SIGS:
+        for beat in (0.5, 0.6):
+            beats, division = _grid(beat, sig)
+            name_to_time, time_to_name, times, bar = ref_encode.get_note_duration_dict(beat, sig)
+            min_diff = name_to_time["sixteenth"] / 2
+            for _ in range(10):
+                raw = _cross_notes(rng, bar, int(rng.integers(1, 9)), beat / division)
+                notes = [PlainNote(*x) for x in raw]
+                ev, carry = ref_encode.bar_notes_to_event(notes, 0.0, bar, np.asarray(beats), time_to_name,
+                                                          times, min_diff, grid_division=division)
+                recs.append({"sig": list(sig), "beat": beat, "beats": beats, "division": division,
+                             "min_diff": min_diff, "bar": float(bar), "notes": raw, "events": ev,
+                             "carry": {str(p): [int(c.pitch), float(c.start), float(c.end), int(c.velocity)]
+                                       for p, c in carry.items()}})
+    assert sum(1 for r in recs if r["carry"]) >= len(recs) // 2
+    return recs
+
+
 if __name__ == "__main__":
     rng = np.random.default_rng(2024)
     out = {"to_category": to_category_cases(rng), "density": density_cases(rng),
            "durations": duration_cases(rng), "grid_notes": grid_cases(rng),
-           "bar_notes_to_event": bar_event_cases(rng)}
+           "bar_notes_to_event": bar_event_cases(rng),
+           "bar_notes_to_event_cross": cross_bar_cases(rng)}
     with open(os.path.join(OUT, "codec_golden.json"), "w") as f:
         json.dump(out, f)
     print("cases:", {k: len(v) if isinstance(v, list) else 1 for k, v in out.items()})

@@ -5,10 +5,12 @@ container with the absent MIDI libraries stubbed as empty modules).
 Pinned here: `_category` (encode.py:206-210), `_density` (13-50),
 `get_note_duration_dict` / `time2durations` (213-277, 947-954),
 `_snap_to_grid` (900-936), `_note_tokens` (939-944) and `_bar_events`
-(957-1141, bars whose notes end inside the bar, continued notes included).
+(957-1141, bars whose notes end inside the bar, continued notes included)
+and its cross-bar continuation branch (1028-1040, 1109-1121: a note running
+past the bar line is cut there and carried to the next bar; the generator
+records the reference's pretty_midi.Note objects with a stub class).
 Still unpinned (they need pretty_midi objects the container lacks):
-`_bar_events`' cross-bar branch (a note running past the bar line is cut
-and carried as a pretty_midi.Note), `event_2midi`, `midi_2event`,
+`event_2midi`, `midi_2event`,
 `encode_midi` and the occupation / polyphony piano-roll statistics;
 tests/test_codec.py checks those by properties."""
 import json
@@ -71,3 +73,17 @@ def test_bar_notes_to_event(k):
                                   c["min_diff"], c["division"])
     assert ev == c["events"]
     assert carry == {}
+
+
+@pytest.mark.parametrize("k", range(len(G["bar_notes_to_event_cross"])))
+def test_bar_notes_to_event_cross_bar(k):
+    """Notes tied over the bar line (`encode.py:1028-1040,1109-1121`): the
+    bar's events and the carried continuations (pitch, start = bar end, end,
+    velocity -1) equal the reference's."""
+    c = G["bar_notes_to_event_cross"][k]
+    _, t2n, times, bar = durations.get_note_duration_dict(c["beat"], tuple(c["sig"]))
+    ev, carry = codec._bar_events(_notes(c["notes"]), 0.0, c["bar"], np.asarray(c["beats"]), t2n, times,
+                                  c["min_diff"], c["division"])
+    assert ev == c["events"]
+    got = {str(p): [int(n.pitch), float(n.start), float(n.end), int(n.velocity)] for p, n in carry.items()}
+    assert got == c["carry"]

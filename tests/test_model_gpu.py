@@ -442,3 +442,57 @@ def test_three_fused_steps_track_oracle(precision, ltol, ptol):
     cap = ptol if precision == "fp32" else 0.5
     bad = {k: e for k, e in errs.items() if e >= cap}
     assert not bad, bad
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_session_graph_after_pe_extension_matches_fresh(golden_dir, precision):
+    """a session's captured step graph addresses the
+    positional table; a second session whose capacities exceed the table
+    extends (reallocates) it.  The first session, replayed afterwards, must
+    not read the freed table: its logits equal those of its first run."""
+    from smer_music_generation_amd.decode import DecodeSession
+    z, meta = _golden(golden_dir)
+    m = _model(z, meta, precision).eval()
+    m.pos_enc.pe = m.pos_enc.pe[:48].clone()
+    srcs = [z["src"][0][:40], z["src"][1][:33]]
+    toks = {r: np.random.default_rng(7 + r).integers(4, 300, 30).tolist() for r in range(2)}
+
+    def run(s):
+        s.prefill([0, 1], srcs)
+        res = []
+        for t in range(20):
+            res.append(s.step([(r, toks[r][t:t + 1], t) for r in range(2)]).copy())
+        return res
+    with torch.no_grad():
+        s1 = DecodeSession(m, 2, 40, 40)
+        first = run(s1)
+        old_ptr = m.pos_enc.pe.data_ptr()
+        s2 = DecodeSession(m, 1, 200, 200)  # extends the table past 48 rows
+        assert m.pos_enc.pe.data_ptr() != old_ptr and m.pos_enc.pe.shape[0] >= 201
+        junk = [torch.full((64, 1, m.pos_enc.pe.shape[2]), 1e4, device=dev) for _ in range(8)]
+        again = run(s1)
+        del junk, s2
+    for a, b in zip(first, again):
+        assert np.array_equal(a, b)
+
+
+def test_fp32_decode_wide_model_unfused_matches_full_forward():
+    """ADVICE r4 (low): the fused fp32 decode layers need d_model <= 2048;
+    a wider model takes the unfused fp32 step, which still equals the full
+    recompute forward."""
+    from smer_music_generation_amd.decode import DecodeSession
+    from smer_music_generation_amd.generation import model_generate
+    from smer_music_generation_amd.model import ScoreTransformer
+    torch.manual_seed(3)
+    d, H = 2112, 33
+    m = ScoreTransformer(309, d, H, 1, 1, 256, 256, 0.0, 0.0, precision="fp32").to(dev).eval()
+    rng = np.random.default_rng(1)
+    src = rng.integers(4, 300, 24)
+    toks = rng.integers(4, 300, 6).tolist()
+    with torch.no_grad():
+        s = DecodeSession(m, 1, 24, 16)
+        s.prefill([0], [src])
+        for t in range(6):
+            got = s.step([(0, toks[t:t + 1], t)])[0]
+        full = model_generate(m, torch.from_numpy(src), toks, dev).numpy()[-1]
+    assert np.abs(got - full).max() < 1e-3
