@@ -196,28 +196,30 @@ def _infill_requests(n, target_len=1024, seed0=0, n_infill_bars=2):
     return reqs
 
 
-def infill_roofline(args, st):
+def infill_roofline(args, st, elem=2):
     """SURVEY.md §8d infill roofline (HBM-bound): every decode step streams
     the decoder weights (L(6d^2 + 2dF) + dV bf16; the cross K/V projections
     ran at prefill) and each live request's K/V rows, L * 2d bf16 per key
     row attended (memory + prefix).  achieved = those bytes / the decode
     loop's wall time."""
     L, d, F, V = args.layers, args.d_model, args.ff, 309
-    w_bytes = (L * (6 * d * d + 2 * d * F) + d * V) * 2
+    w_bytes = (L * (6 * d * d + 2 * d * F) + d * V) * elem
     if not st.get("kv_row_reads") or not st.get("step_call_s"):
         return None
-    total = st["steps"] * w_bytes + st["kv_row_reads"] * L * 2 * d * 2
+    total = st["steps"] * w_bytes + st["kv_row_reads"] * L * 2 * d * elem
     gbs = total / st["step_call_s"] / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": round(total / max(1, st["steps"])),
             "weight_bytes_per_step": w_bytes}
 
 
-def bench_infill(args, dev, rank):
+def bench_infill(args, dev, rank, precision="bf16"):
+    """precision "fp32": the bit-exact decode path (greedy ids equal the
+    reference's; tests/test_prod_gpu.py), same requests and method."""
     from smer_music_generation_amd.generation import generation_batch
     from smer_music_generation_amd.vocab import WordVocab
     v = WordVocab(0, CTRL)
-    m = make_model(args, dev).eval()
+    m = make_model(args, dev, precision).eval()
     all_controls = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
     # the first call (other requests, sources a little longer) allocates the
     # session and captures the decode graph: timed as the cold rate; the
@@ -246,7 +248,7 @@ def bench_infill(args, dev, rank):
                              **{k: round(v, 4) for k, v in st.get("decode_phases_s", {}).items()}),
             "tokens_per_s": st["tokens"] / dt, "requests": len(reqs), "mean_src_len": src_len,
             "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
-            "roofline": infill_roofline(args, st)}
+            "roofline": infill_roofline(args, st, 4 if precision == "fp32" else 2)}
 
 
 def bench_infill_batch1(args, dev, rank):
@@ -287,7 +289,7 @@ def bench_infill_batch1(args, dev, rank):
             "warm_call_s_mean": round(dt / len(reqs), 4)}
 
 
-def bench_infill_c5(args, dev, rank):
+def bench_infill_c5(args, dev, rank, precision="bf16"):
     """BASELINE.json configs[4]: 64 concurrent requests,
     sources of ~4096 SMER tokens, each infilling 4 bars of one track, greedy,
     KV-cached, graph-captured decode step with the grammar on device.
@@ -296,7 +298,7 @@ def bench_infill_c5(args, dev, rank):
     from smer_music_generation_amd.generation import generation_batch
     from smer_music_generation_amd.vocab import WordVocab
     v = WordVocab(0, CTRL)
-    m = make_model(args, dev).eval()
+    m = make_model(args, dev, precision).eval()
     all_controls = v.density_indices + v.occupation_indices + v.polyphony_indices + v.tensile_indices
     # cold first call on other requests (session + graph capture), then the
     # timed call on the warm session (see bench_infill)
@@ -319,7 +321,7 @@ def bench_infill_c5(args, dev, rank):
             "p50_latency_s": float(np.percentile(lat, 50)),
             "p90_latency_s": float(np.percentile(lat, 90)),
             "ms_per_decode_step": 1000 * st["step_call_s"] / max(1, st["steps"]),
-            "roofline": infill_roofline(args, st),
+            "roofline": infill_roofline(args, st, 4 if precision == "fp32" else 2),
             "phases_s": dict({k: round(st[k], 4) for k in ("prepare_s", "prefill_s", "decode_s")},
                              **{k: round(v, 4) for k, v in st.get("decode_phases_s", {}).items()})}
 
@@ -403,6 +405,13 @@ def cpu_baseline(args):
     return res
 
 
+# every bf16 GEMM tile kernel behind ops.gemm / gemm_wgrad_bias (the calls
+# the live HIP-event timer brackets); the split-K reduce is added per call
+GEMM_FAMILY = ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm256s_bf16_kernel",
+               "gemm256_wgrad_kernel", "gemm256s_wgrad_kernel", "gemm64_bf16_kernel",
+               "gemm_skinny_bf16_kernel")
+
+
 def _pmc_traffic():
     """HBM bytes per gemm_bf16_kernel launch (FETCH_SIZE x2 + WRITE_SIZE,
     launch-weighted over the three layout variants) from the newest committed
@@ -417,8 +426,7 @@ def _pmc_traffic():
     # the smer_gemm family: 128x128 and 256x256 tile kernels, skinny kernel,
     # split-K slab reduction (one smer_gemm call = tile kernel [+ reduce])
     s = {(k[5:] if k.startswith("void ") else k): v for k, v in s.items()}
-    g = [v for k, v in s.items() if k.startswith(("gemm_bf16_kernel", "gemm256_bf16_kernel",
-                                                    "gemm64_bf16_kernel", "gemm_skinny_bf16_kernel"))]
+    g = [v for k, v in s.items() if k.startswith(GEMM_FAMILY)]
     n = sum(v["launches"] for v in g)
     if not n:
         return None
@@ -449,6 +457,8 @@ def parse_args(argv=None):
     ap.add_argument("--c4-warmup", dest="c4_warmup", type=int, default=1)
     ap.add_argument("--c5-requests", dest="c5_requests", type=int, default=64)
     ap.add_argument("--c5-seq", dest="c5_seq", type=int, default=4096)
+    ap.add_argument("--no-fp32-infill", dest="fp32_infill", action="store_false",
+                    help="skip the fp32 (bit-exact) batched greedy infill lines at C2 and C5")
     ap.add_argument("--no-cpu", dest="cpu", action="store_false")
     ap.add_argument("--no-roofline", dest="roofline", action="store_false")
     ap.add_argument("--grad-wire", dest="grad_wire", choices=("fp32", "bf16"), default="fp32",
@@ -646,6 +656,16 @@ def main():
             sec = torch.tensor([c5["seconds"]], device=dev, dtype=torch.float64)
             dist.all_reduce(sec, op=dist.ReduceOp.MAX)
             c5["tokens_per_s"] = t.item() / sec.item()
+    # the bit-exact decode path (fp32; greedy ids equal the reference's),
+    # same requests and method as the bf16 lines above
+    inf32 = c5_32 = None
+    if args.infill and args.fp32_infill:
+        torch.cuda.empty_cache()
+        inf32 = bench_infill(args, dev, rank, "fp32")
+        if args.c5:
+            torch.cuda.empty_cache()
+            c5_32 = bench_infill_c5(args, dev, rank, "fp32")
+        torch.cuda.empty_cache()
     cpu = cpu_baseline(args) if (args.cpu and rank == 0 and world == 1) else None
     feed = data_feed(tr["tokens_per_s"] / world) if (args.cpu and rank == 0) else None
 
@@ -653,7 +673,9 @@ def main():
         roof = None
         if "gemm" in tr:
             g = tr["gemm"]
-            roof = {"bound": "mfma", "kernel": "gemm_bf16_kernel (smer_gemm)",
+            roof = {"bound": "mfma",
+                    "kernel": "smer_gemm family (%s + splitk_reduce_kernel): achieved, frac "
+                              "and traffic all over this set" % ", ".join(GEMM_FAMILY),
                     "achieved": round(g["tflops"], 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(g["tflops"] / BF16_PEAK_TFLOPS, 4), "traffic": (_pmc_traffic() or {}).get("bytes_per_launch"),
                     "traffic_unit": "HBM bytes per launch (rocprofv3 PMC)",
@@ -732,6 +754,25 @@ def main():
                                  "decode_steps": c5["steps"], "tokens": c5["tokens"],
                                  "roofline": c5["roofline"],
                                  "phases_s": c5["phases_s"], "parallelism": "replicas"},
+            "infill_fp32": inf32 and {
+                "metric": "infill tokens/s on the bit-exact fp32 decode path (greedy ids equal "
+                          "the reference's), C2 requests as `infill`, warm session",
+                "value": round(inf32["tokens_per_s"], 1),
+                "cold_value": round(inf32["cold_tokens_per_s"], 1),
+                "ms_per_decode_step": round(inf32["ms_per_decode_step"], 3),
+                "decode_steps": inf32["steps"], "tokens": inf32["tokens"],
+                "roofline": inf32["roofline"], "phases_s": inf32["phases_s"],
+                "per_rank": True},
+            "infill_c5_fp32": c5_32 and {
+                "metric": "C5 batched infill tokens/s on the bit-exact fp32 decode path, "
+                          "requests as `infill_c5`, warm session",
+                "value": round(c5_32["tokens_per_s"], 1),
+                "cold_value": round(c5_32["cold_tokens_per_s"], 1),
+                "p50_latency_s": round(c5_32["p50_latency_s"], 4),
+                "ms_per_decode_step": round(c5_32["ms_per_decode_step"], 3),
+                "decode_steps": c5_32["steps"], "tokens": c5_32["tokens"],
+                "roofline": c5_32["roofline"], "phases_s": c5_32["phases_s"],
+                "per_rank": True},
             "cpu_baseline": cpu,
             "data_pipeline": feed,
         }

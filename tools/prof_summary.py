@@ -13,9 +13,12 @@ for r in sorted(rows, key=lambda r: -float(r['TotalDurationNs']))[:int(sys.argv[
                                           float(r['TotalDurationNs']) / 1e6 / steps,
                                           100 * float(r['TotalDurationNs']) / tot))
 print("total kernel time per step: %.3f ms" % (tot / 1e6 / steps))
-fam = [r for r in rows if r['Name'].replace('void ', '').startswith(
-    ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm64_bf16_kernel",
-     "gemm_skinny_bf16_kernel"))]
+# every GEMM tile kernel of the product (bf16 and fp8; bench.py GEMM_FAMILY
+# is the bf16 subset the live roofline times)
+FAMILY = ("gemm_bf16_kernel", "gemm256_bf16_kernel", "gemm256s_bf16_kernel", "gemm256_wgrad_kernel",
+          "gemm256s_wgrad_kernel", "gemm64_bf16_kernel", "gemm_skinny_bf16_kernel",
+          "gemm256_fp8_kernel", "gemm256s_fp8_kernel")
+fam = [r for r in rows if r['Name'].replace('void ', '').startswith(FAMILY)]
 red = [r for r in rows if r['Name'].startswith("splitk_reduce_kernel")]
 if fam:
     calls = sum(int(r['Calls']) for r in fam)
