@@ -117,10 +117,11 @@ int smer_gemm_debug_stamps(void* buf);
  * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:
  * key j visible to query i iff j <= i.  lse: fp32 [B, H, Lq] (natural log).
  * Attention-probability dropout with (drop_p, seed). */
-/* Attention-dropout keep bits of a [B*H, Lq, Lk] score matrix, exactly the
- * words smer_attn_fwd publishes when it hashes them itself (layout: see
- * smer_attn_drop_mask_bytes); smer_attn_fwd(..., drop_mask, drop_mask_in = 1)
- * then reads them instead of hashing (the forward is VALU-bound). */
+/* Attention-dropout keep bits of a [B*H, Lq, Lk] score matrix (layout: see
+ * smer_attn_drop_mask_bytes), the same keep decisions the forward hashes in
+ * its loop when it gets no mask buffer; smer_attn_fwd(..., drop_mask,
+ * drop_mask_in = 1) reads them (the forward is VALU-bound), and so does
+ * smer_attn_bwd. */
 int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_p, uint32_t seed, void* mask,
                             smer_stream_t stream);
 int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D,
@@ -128,11 +129,12 @@ int smer_attn_fwd(int dtype, int B, int H, int Lq, int Lk, int D,
                   void* o, long ldo, float* lse, const uint8_t* kpm, int causal, float scale,
                   float drop_p, uint32_t seed, void* drop_mask, int drop_mask_in,
                   smer_stream_t stream);
-/* drop_mask (nullable, 16-B aligned, smer_attn_drop_mask_bytes): with
- * drop_p > 0 the bf16 forward also stores its keep bits (1 bit per
- * (query, key), as four 64-bit wave ballots per 16x16 block) so that
- * smer_attn_bwd reads them instead of re-hashing; the mask is the same
- * either way. */
+/* drop_mask (nullable, 16-B aligned, smer_attn_drop_mask_bytes bytes: one
+ * u32 per (b*H+h, 32-query block, 64-key tile, lane), 1 bit per (query,
+ * key)): with drop_p > 0 and drop_mask_in = 0 the bf16 forward first fills
+ * it (smer_attn_drop_mask_gen on the same stream), then reads it, and so does
+ * smer_attn_bwd given the same buffer; NULL: the forward and the backward
+ * hash the keep bits in their loops.  The mask is the same either way. */
 size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk);
 size_t smer_attn_bwd_workspace(int dtype, int B, int H, int Lq, int Lk);
 int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D,

@@ -131,15 +131,36 @@ __device__ __forceinline__ float max_4groups(float x) {
 }
 }  // namespace
 
-// Attention-dropout keep words (forward publishes, backward reads): 16 bits
-// per (query 16-block q16, key 64-tile t, forward lane (g, c)); bit 4r + mt
-// = keep of (query 16*q16 + c, key 64t + 16mt + 4g + r), i.e. byte r of
-// smer_attn_bits(rowkey(query), quad 16t + 4mt + g).  Built from the SWAR
-// compare words ge_mt (bit 8r + 7 per key): OR_mt ge_mt >> (7 - mt) puts
-// key (mt, r) at bit 8r + mt; folding the four nibbles gives 4r + mt.
-__device__ __forceinline__ uint32_t attn_fold_keep(uint32_t acc) {
-  const uint32_t y = acc | (acc >> 4);
-  return (y & 0xFFu) | ((y >> 8) & 0xFF00u);
+// Attention-dropout keep words, generated once per attention call by
+// attn_drop_mask_gen_kernel (full occupancy, pure integer VALU) and read by
+// the forward and both backward kernels: one u32 per (bh, query 32-block
+// q32, key 64-tile t, forward lane (G, c)); bit 8R + 4gq + mt = keep of
+// (query 32*q32 + 16*gq + c, key 64t + 16mt + 4G + R), i.e. byte R of the
+// SWAR compare of smer_attn_bits(rowkey(query), quad 16t + 4mt + G).  The
+// byte-major order lets the forward turn a word into the 16-bit AND masks of
+// its packed bf16 P pairs with one v_perm per key pair (r, r+1) and a shift
+// + arithmetic shift per (gq, mt) (attn_pair_mask).
+__device__ __forceinline__ uint32_t attn_mask_word(uint32_t rk0, uint32_t rk1, uint32_t t, uint32_t G,
+                                                   uint32_t lo4) {
+  uint32_t w = 0u;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const uint32_t quad = t * (KVB / 4) + 4 * mt + G;
+    w |= ((smer_attn_ge(smer_attn_bits(rk0, quad), lo4) >> 7) & 0x01010101u) << mt;
+    w |= ((smer_attn_ge(smer_attn_bits(rk1, quad), lo4) >> 7) & 0x01010101u) << (4 + mt);
+  }
+  return w;
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// pw = perm(word) holding key r's byte in the low 16-bit half and key r+1's
+// in the high half (both bytes of each half): AND masks (0xFFFF / 0) of the
+// pair's two bf16 halves from bit k of each byte
+__device__ __forceinline__ uint32_t attn_pair_mask(uint32_t pw, uint32_t k) {
+  const u16x2 x = __builtin_bit_cast(u16x2, pw) << (unsigned short)(15u - k);
+  return half_masks(__builtin_bit_cast(uint32_t, x));
+}
+__device__ __forceinline__ size_t attn_mask_index(int bh, int nq32, int nkt, int q32, int t) {
+  return (((size_t)bh * nq32 + q32) * nkt + t) * 64;
 }
 
 // ---------------------------------------------------------------------------
@@ -162,12 +183,12 @@ struct AttnQ8 {
 // QG query groups of 16 per wave (block = 64*QG queries): K / V fragments
 // read from LDS once per wave feed QG groups, halving LDS traffic per MFMA
 // at QG = 2 (the forward is otherwise LDS-bandwidth co-limited).
-// MIN: the keep words come precomputed (attn_drop_mask_gen_kernel) instead
-// of being hashed here (measured: the separate generator costs more than the
-// hashing it saves; kept as a tested building block).
-// Dropout (DROP): per lane and key tile 4 hashes (one per quad of keys),
-// SWAR byte compares, AND masks on the packed bf16 P -- about 20 VALU
-// instructions per 16 scores besides the softmax.
+// MIN: the keep words come precomputed (attn_drop_mask_gen_kernel, the
+// product path whenever the caller keeps the mask for the backward): one
+// word per lane and key tile, prefetched a tile ahead, 3 VALU per packed P
+// pair.  Hashing in the loop instead (DROP && !MIN, only when the caller
+// passes no mask buffer) costs 4 hashes per lane and key tile plus SWAR
+// compares: it made the C2 encoder forward 42 % slower (99.6 -> 141.6 us).
 // Q8: also the e4m3 copy of O (q8.dq; C4 fp8), a separate instance so that
 // the plain forward's code is untouched by it
 template <int D, int QG, bool DROP, bool MIN = false, bool Q8 = false>
@@ -235,7 +256,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
   f32x4 acc[QG][C::NDT];
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
-    rowkey[gq] = DROP ? smer_rowkey(seed, (uint32_t)(bh * Lq + q0w + gq * 16 + c16)) : 0u;
+    rowkey[gq] = (DROP && !MIN) ? smer_rowkey(seed, (uint32_t)(bh * Lq + q0w + gq * 16 + c16)) : 0u;
     m_run[gq] = -INFINITY;
     m_ref[gq] = 0.f;
     negm[gq] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -248,7 +269,20 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
   auto key_bias = [&](int key) -> float {
     return (key >= Lk || (kp && kp[key])) ? -INFINITY : 0.f;
   };
+  // MIN: this wave's keep words (its 16 * QG queries lie in one 32-query
+  // block; gq_k = the 16-query half of a QG = 1 wave), one per key tile
+  const int nq32 = (Lq + 31) >> 5;
+  const uint32_t* mwp = (DROP && MIN)
+      ? reinterpret_cast<const uint32_t*>(drop_mask) + attn_mask_index(bh, nq32, nkt, min(q0w >> 5, nq32 - 1), 0) + lane
+      : nullptr;
+  const uint32_t gq_k = QG == 2 ? 0u : (uint32_t)((q0w >> 4) & 1);
+  uint32_t mw_next = 0u;
+  // hashing (QG = 2) with a buffer: the keep words it publishes
+  uint32_t* mwo = (DROP && !MIN && QG == 2 && drop_mask && (q0w >> 5) < nq32)
+      ? reinterpret_cast<uint32_t*>(drop_mask) + attn_mask_index(bh, nq32, nkt, q0w >> 5, 0) + lane
+      : nullptr;
   if (n_tiles > 0) {
+    if constexpr (DROP && MIN) mw_next = mwp[0];
     tile_load<D>(rk, kb, ldk, 0, Lk, tid);
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
@@ -282,13 +316,9 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
-    uint32_t mw[QG];
+    uint32_t mw = mw_next;
     if constexpr (DROP && MIN) {
-#pragma unroll
-      for (int gq = 0; gq < QG; ++gq) {
-        const int q16 = min((q0w + gq * 16) >> 4, nq16 - 1);
-        mw[gq] = reinterpret_cast<const uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane];
-      }
+      if (more) mw_next = mwp[(size_t)(t + 1) * 64];
     }
     f32x4 st[QG][4];
 #pragma unroll
@@ -312,6 +342,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       }
     }
     bf16x8 pf[QG][2];
+    uint32_t kword = 0u;
 #pragma unroll
     for (int gq = 0; gq < QG; ++gq) {
       const int qi = q0w + gq * 16 + c16;
@@ -369,18 +400,20 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
         pw[mt][1] = pack2(p[mt][2], p[mt][3]);
       }
       if (DROP && MIN) {
-        const int q16 = (q0w + gq * 16) >> 4;
-        const uint32_t mword = min(q16, nq16 - 1) == q16 ? mw[gq] : 0u;
+        // bytes [r0 r0 r1 r1] / [r2 r2 r3 r3] of the word; bit 4gq + mt of
+        // each byte shifted to its half's sign and smeared over the half
+        const uint32_t p01 = __builtin_amdgcn_perm(mw, mw, 0x01010000u);
+        const uint32_t p23 = __builtin_amdgcn_perm(mw, mw, 0x03030202u);
+        const uint32_t kq = 4u * (QG == 2 ? (uint32_t)gq : gq_k);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int rp = 0; rp < 2; ++rp)
-            pw[mt][rp] &= (bitmask32(mword, 8 * rp + mt) & 0xFFFFu) |
-                          (bitmask32(mword, 8 * rp + 4 + mt) & 0xFFFF0000u);
+        for (int mt = 0; mt < 4; ++mt) {
+          pw[mt][0] &= attn_pair_mask(p01, kq + mt);
+          pw[mt][1] &= attn_pair_mask(p23, kq + mt);
+        }
       } else if (DROP) {
         // one hash per quad of keys (16mt + 4g .. +3): byte r decides key r
         const uint32_t quad0 = (uint32_t)(t * (KVB / 4) + g);
-        uint32_t kacc = 0u;
+        const uint32_t kq = 4u * (QG == 2 ? (uint32_t)gq : gq_k);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const uint32_t ge = smer_attn_ge(smer_attn_bits(rowkey[gq], quad0 + 4 * mt), lo4);
@@ -388,15 +421,16 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
           // sign (the keep bit) smeared over the half
           pw[mt][0] &= half_masks(__builtin_amdgcn_perm(ge, ge, 0x01010000u));
           pw[mt][1] &= half_masks(__builtin_amdgcn_perm(ge, ge, 0x03030202u));
-          kacc |= (ge >> (7 - mt)) & (0x01010101u << mt);
+          if (QG == 2) kword |= ((ge >> 7) & 0x01010101u) << (kq + mt);
         }
-        const int q16 = (q0w + gq * 16) >> 4;
-        if (drop_mask && q16 < nq16)
-          reinterpret_cast<uint16_t*>(drop_mask)[(((long)bh * nq16 + q16) * nkt + t) * 64 + lane] =
-              (uint16_t)attn_fold_keep(kacc);
       }
       pf[gq][0] = words_bf16x8(pw[0][0], pw[0][1], pw[1][0], pw[1][1]);
       pf[gq][1] = words_bf16x8(pw[2][0], pw[2][1], pw[3][0], pw[3][1]);
+    }
+    // hashing forward with a mask buffer (QG = 2: the wave's 32 queries are
+    // one 32-query block): publish the tile's keep word for the backward
+    if constexpr (DROP && !MIN && QG == 2) {
+      if (mwo) __builtin_nontemporal_store(kword, mwo + (size_t)t * 64);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -484,9 +518,9 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   __shared__ __attribute__((aligned(16))) float s_lse[2][KVB];
   __shared__ __attribute__((aligned(16))) float s_del[2][KVB];
   __shared__ __attribute__((aligned(16))) uint32_t s_rk[2][KVB];
-  // forward's keep words of the staged query tile x this block's key tiles:
-  // [query 16-block][key tile][64 lanes] (16 bits each)
-  __shared__ __attribute__((aligned(16))) uint16_t s_msk[2][4][KG][64];
+  // keep words of the staged query tile x this block's key tiles:
+  // [query 32-block][key tile][64 forward lanes] (attn_mask_word)
+  __shared__ __attribute__((aligned(16))) uint32_t s_msk[2][2][KG][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
@@ -529,12 +563,13 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   float rl = 0.f, rd = 0.f;
   uint32_t rr = 0u;
   uint4 rm = make_uint4(0, 0, 0, 0);
-  constexpr int MCH = KG * 128 / 16;  // 16-B chunks per query 16-block row
   constexpr bool use_mask = DROP && MSK;
-  // this thread's mask chunk: query 16-block t*4 + m_qr, key tile m_kt
-  const int m_qr = tid / MCH, m_ch = tid % MCH, m_kt = BX * KG + m_ch / 8;
+  // this thread's 16-B chunk m_ch of the words of (query 32-block 2t + m_qr,
+  // key tile m_kt): 2 x KG x 16 chunks per query tile
+  const int nq32 = (Lq + 31) >> 5;
+  const int m_qr = tid / (16 * KG), m_kt = BX * KG + (tid / 16) % KG, m_ch = tid & 15;
   const uint4* m_base = use_mask ? reinterpret_cast<const uint4*>(drop_mask) +
-                                       ((long)bh * nq16 * nkt + m_kt) * 8 + (m_ch & 7)
+                                       (attn_mask_index(bh, nq32, nkt, 0, min(m_kt, nkt - 1)) >> 2) + m_ch
                                  : nullptr;
   auto load = [&](int t) {
     tile_load<D>(rq, qb, ldq, t * KVB, Lq, tid);
@@ -547,9 +582,9 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       rd = db[min(qq, Lq - 1)];
       if (DROP && !MSK) rr = smer_rowkey(seed, (uint32_t)(bh * Lq + qq));
     }
-    if (use_mask && tid < 4 * MCH) {
-      const int q16 = t * 4 + m_qr;
-      rm = (q16 < nq16 && m_kt < nkt) ? m_base[q16 * nkt * 8] : make_uint4(0, 0, 0, 0);
+    if (use_mask && tid < 32 * KG) {
+      const int q32 = t * 2 + m_qr;
+      rm = (q32 < nq32 && m_kt < nkt) ? m_base[(size_t)q32 * nkt * 16] : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&](int buf, int t) {
@@ -562,7 +597,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       s_del[buf][tid] = qv ? rd : 0.f;
       if (DROP && !MSK) s_rk[buf][tid] = rr;
     }
-    if (use_mask && tid < 4 * MCH)
+    if (use_mask && tid < 32 * KG)
       reinterpret_cast<uint4*>(&s_msk[buf][0][0][0])[tid] = rm;
   };
   if (t0 < n_qt) { load(t0); store(0, t0); }
@@ -607,17 +642,17 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
           dpacc = mfma16(row_frag<D>(Os, mt * 16, s, lane), vf[gk][s], dpacc);
         }
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(&s_del[cur][mt * 16 + 4 * g]);
-        // forward lane (G, c) of word [q16][key tile] holds (query c, key
-        // 16*mk + 4G + R) at bit 4R + mk: this lane (key c16 of 16-block k16,
-        // queries 4g..4g+3 of block mt) reads the words of lanes
-        // 16*(c16>>2) + 4g .. +3 (one 8-B read), bit 4*(c16&3) + (k16&3)
-        uint32_t mlo = 0u, mhi = 0u;
+        // forward lane (G, c) of word [q32][key tile] holds (query 16gq + c,
+        // key 16*mk + 4G + R) at bit 8R + 4gq + mk: this lane (key c16 of
+        // 16-block k16, queries 4g..4g+3 of 16-block mt) reads the words of
+        // lanes 16*(c16>>2) + 4g .. +3 (one 16-B read), bit
+        // 8*(c16&3) + 4*(mt&1) + (k16&3)
+        uint4 mw4 = make_uint4(0, 0, 0, 0);
         if constexpr (use_mask) {
           const int j = (k16 >> 2) - BX * KG;
-          const uint64_t w = *reinterpret_cast<const uint64_t*>(&s_msk[cur][mt][j][(c16 >> 2) * 16 + 4 * g]);
-          mlo = (uint32_t)w;
-          mhi = (uint32_t)(w >> 32);
+          mw4 = *reinterpret_cast<const uint4*>(&s_msk[cur][mt >> 1][j][(c16 >> 2) * 16 + 4 * g]);
         }
+        const uint32_t mbit = 8 * (c16 & 3) + 4 * (mt & 1) + (k16 & 3);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float pv = fast_exp2(sacc[r]);
@@ -627,7 +662,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
           if (DROP) {
             uint32_t m;
             if constexpr (use_mask) {
-              m = bitmask32(r < 2 ? mlo : mhi, 16 * (r & 1) + 4 * (c16 & 3) + (k16 & 3));
+              m = bitmask32(r == 0 ? mw4.x : r == 1 ? mw4.y : r == 2 ? mw4.z : mw4.w, mbit);
             } else {
               m = smer_attn_keep(s_rk[cur][mt * 16 + 4 * g + r], drop_thr, (uint32_t)kj) ? ~0u : 0u;
             }
@@ -715,9 +750,6 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   __shared__ __attribute__((aligned(16))) char sm[2][2][C::TILE];
   __shared__ __attribute__((aligned(16))) float kbias[2][KVB];
   __shared__ int kpad[2];  // the staged tile has a padded / out-of-range key
-  // forward's keep words: [query 16-block of the block][lane] for the
-  // staged key tile (16 bits each, the forward's own lane mapping)
-  __shared__ __attribute__((aligned(16))) uint16_t s_msk[2][4 * QG][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   int BX, BY;
@@ -726,14 +758,15 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
   const int q0w = BX * QB + wave * 16 * QG;  // first query of this wave
   const float c = scale * LOG2E_F;
   constexpr bool use_mask = DROP && MSK;
-  // 16-B chunk `ch` of the block's mask words for key tile t (8 per q16)
-  const int m_q16 = (BX * QB >> 4) + (tid >> 3);
-  const uint4* m_base = use_mask ? reinterpret_cast<const uint4*>(drop_mask) +
-                                       ((long)bh * nq16 + m_q16) * nkt * 8 + (tid & 7)
-                                 : nullptr;
-  auto mask_load = [&](int t, int ch) -> uint4 {
-    return m_q16 < nq16 ? m_base[t * 8] : make_uint4(0, 0, 0, 0);
-  };
+  // this wave's keep words (the forward's lane mapping: one word per lane
+  // and key tile, its 16 * QG queries inside one 32-query block), prefetched
+  // a tile ahead in a register
+  const int nq32 = (Lq + 31) >> 5;
+  const uint32_t* mwp = use_mask
+      ? reinterpret_cast<const uint32_t*>(drop_mask) + attn_mask_index(bh, nq32, nkt, min(q0w >> 5, nq32 - 1), 0) + lane
+      : nullptr;
+  const uint32_t gq_k = QG == 2 ? 0u : (uint32_t)((q0w >> 4) & 1);
+  uint32_t mw_next = 0u;
   bf16x8 qf[QG][C::NS], of[QG][C::NS], ovr[QG][C::NS];
   float lse2[QG], dlt[QG];
   uint32_t rowkey[QG];
@@ -782,7 +815,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
       const uint64_t any = __ballot(kbz != 0.f);
       if (tid == 0) kpad[0] = any != 0ull;
     }
-    if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[0][0][0])[tid] = mask_load(0, tid);
+    if constexpr (use_mask) mw_next = mwp[0];
   }
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
@@ -825,12 +858,12 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     const int cur = t & 1;
     const bool more = t + 1 < n_tiles;
     int npad = 0;  // compared when staged (see attn_fwd_bf16)
-    uint4 nmask = make_uint4(0, 0, 0, 0);
+    const uint32_t mw = mw_next;
     if (more) {
       tile_load<D>(rk, kb, ldk, (t + 1) * KVB, Lk, tid);
       tile_load<D>(rv, vb, ldv, (t + 1) * KVB, Lk, tid);
       if (kp) npad = kp[min((t + 1) * KVB + lane, Lk - 1)];  // every lane: no exec-masked join
-      if (use_mask && tid < 32 * QG) nmask = mask_load(t + 1, tid);
+      if constexpr (use_mask) mw_next = mwp[(size_t)(t + 1) * 64];
     }
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
@@ -874,10 +907,10 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) dpv[r] = dpacc[gq][mt][r];
         if constexpr (use_mask) {
-          // same lane mapping as the forward: bit 4r + mt of this lane's word
-          const uint32_t w = s_msk[cur][((q0w - BX * QB) >> 4) + gq][lane];
+          // same lane mapping as the forward: bit 8r + 4gq + mt of the word
+          const uint32_t kq = 4u * (QG == 2 ? (uint32_t)gq : gq_k) + mt;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dpv[r] = and_f32(dpv[r], bitmask32(w, 4 * r + mt));
+          for (int r = 0; r < 4; ++r) dpv[r] = and_f32(dpv[r], bitmask32(mw, 8 * r + kq));
         } else if (DROP) {
           const uint32_t hb = smer_attn_bits(rowkey[gq], (uint32_t)(t * (KVB / 4) + mt * 4 + g));
 #pragma unroll
@@ -913,7 +946,6 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
         const uint64_t any = __ballot(pk);
         if (tid == 0) kpad[cur ^ 1] = any != 0ull;
       }
-      if (use_mask && tid < 32 * QG) reinterpret_cast<uint4*>(&s_msk[cur ^ 1][0][0])[tid] = nmask;
     }
     __syncthreads();
   }
@@ -1664,29 +1696,30 @@ __global__ void kv_scatter_heads_kernel(int n_rows, int H, int D, const T* __res
       *reinterpret_cast<const uint4*>(src + (long)m * lds + col);
 }
 
-// The attention-dropout keep words of a whole [B*H, Lq, Lk] score matrix,
-// bit for bit what attn_fwd_bf16 (hashing path) publishes (layout: see
-// attn_fold_keep).  Pure integer VALU at full occupancy.
-__global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(long nwords, int Lq, int nq16, int nkt,
-                                                                uint32_t thr, uint32_t seed,
-                                                                uint16_t* __restrict__ out) {
-  const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nwords) return;
-  const int lane = (int)(w & 63);
-  const long rest = w >> 6;
-  const int t = (int)(rest % nkt);
-  const long r2 = rest / nkt;
-  const int q16 = (int)(r2 % nq16);
-  const long bh = r2 / nq16;
-  const int g = lane >> 4, c = lane & 15;
+// The attention-dropout keep words of a whole [B*H, Lq, Lk] score matrix
+// (layout: attn_mask_word).  One wave per (bh, query 32-block): each lane
+// hashes its two row keys once and walks every key tile, 8 hashes and one
+// 4-B store per tile (long-lived waves: a wave per (block, tile) spent as
+// long in dispatch as in its 100 VALU instructions).  Pure integer VALU at
+// full occupancy; no division anywhere.
+__global__ __launch_bounds__(256) void attn_drop_mask_gen_kernel(int Lq, int nq32, int nkt, uint32_t thr,
+                                                                uint32_t seed, uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int q32 = blockIdx.x * 4 + (threadIdx.x >> 6), bh = blockIdx.y;
+  if (q32 >= nq32) return;
+  const uint32_t row0 = (uint32_t)bh * (uint32_t)Lq + (uint32_t)(q32 * 32 + (lane & 15));
+  const uint32_t rk0 = smer_rowkey(seed, row0), rk1 = smer_rowkey(seed, row0 + 16u);
   const uint32_t lo4 = thr * 0x01010101u;
-  const uint32_t rowkey = smer_rowkey(seed, (uint32_t)(bh * Lq + q16 * 16 + c));
-  const uint32_t quad0 = (uint32_t)(t * (KVB / 4) + g);
-  uint32_t acc = 0u;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-    acc |= (smer_attn_ge(smer_attn_bits(rowkey, quad0 + 4 * mt), lo4) >> (7 - mt)) & (0x01010101u << mt);
-  out[w] = (uint16_t)attn_fold_keep(acc);
+  uint32_t* o = out + attn_mask_index(bh, nq32, nkt, q32, 0) + lane;
+  for (int t = 0; t < nkt; ++t)
+    __builtin_nontemporal_store(attn_mask_word(rk0, rk1, (uint32_t)t, (uint32_t)(lane >> 4), lo4), o + (size_t)t * 64);
+}
+
+static void mask_gen_launch(int B, int H, int Lq, int Lk, uint32_t thr, uint32_t seed, void* mask,
+                            hipStream_t s) {
+  const int nq32 = (Lq + 31) / 32, nkt = (Lk + 63) / 64;
+  hipLaunchKernelGGL(attn_drop_mask_gen_kernel, dim3((nq32 + 3) / 4, B * H), dim3(256), 0, s, Lq, nq32, nkt,
+                     thr, seed, (uint32_t*)mask);
 }
 
 // ---------------------------------------------------------------------------
@@ -1703,37 +1736,45 @@ static void fwd_bf16_launch(int B, int H, int Lq, int Lk, const void* q, long ld
   // two query groups per wave once there are enough blocks to fill the chip
   const bool qg2 = (long)((Lq + 127) / 128) * B * H >= 512 && D <= 64;
   dim3 grid(qg2 ? (Lq + 127) / 128 : (Lq + 63) / 64, B * H);
-  const bool min_ = thr && mask && mask_in;
+  // a mask buffer: the keep words come from the generator (launched here
+  // first unless the caller already filled them) and the backward reads the
+  // same words; no buffer: the forward hashes them itself
+  // with a mask buffer the QG = 2 forward hashes the keep bits in its loop
+  // and publishes them (cheaper than the separate generator: C2 encoder
+  // forward + generator 125 + 29 us vs ~14x us hashing + publishing); a
+  // QG = 1 wave holds half a 32-query block, so there the generator fills
+  // the buffer and the forward reads it
+  const bool min_ = thr && mask && (mask_in || !qg2);
+  if (min_ && !mask_in) mask_gen_launch(B, H, Lq, Lk, thr, seed, mask, s);
   auto kern = qg2 ? (min_ ? attn_fwd_bf16<D, 2, true, true>
                           : (thr ? attn_fwd_bf16<D, 2, true> : attn_fwd_bf16<D, 2, false>))
                   : (min_ ? attn_fwd_bf16<D, 1, true, true>
                           : (thr ? attn_fwd_bf16<D, 1, true> : attn_fwd_bf16<D, 1, false>));
   if constexpr (D == 64) {
-    if (q8.dq)  // (the C-ABI rejects a copy with precomputed keep bits)
-      kern = qg2 ? (thr ? attn_fwd_bf16<D, 2, true, false, true> : attn_fwd_bf16<D, 2, false, false, true>)
-                 : (thr ? attn_fwd_bf16<D, 1, true, false, true> : attn_fwd_bf16<D, 1, false, false, true>);
+    if (q8.dq)
+      kern = qg2 ? (min_ ? attn_fwd_bf16<D, 2, true, true, true>
+                         : (thr ? attn_fwd_bf16<D, 2, true, false, true> : attn_fwd_bf16<D, 2, false, false, true>))
+                 : (min_ ? attn_fwd_bf16<D, 1, true, true, true>
+                         : (thr ? attn_fwd_bf16<D, 1, true, false, true> : attn_fwd_bf16<D, 1, false, false, true>));
   }
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, B, H, Lq, Lk, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, lse, kpm, causal,
-                     scale, thr, seed, ds, thr ? mask : nullptr, q8);
+                     scale, thr, seed, ds, thr ? (uint64_t*)mask : nullptr, q8);
 }
 
-// [bh][query 16-block][key 64-tile][64 lanes] 16-bit words: lane (g, c) of
-// the forward's wave holds (query 16*q16 + c, key 64*t + 16*mt + 4g + r) at
-// bit 4r + mt.  1 bit per (query, key).
+// [bh][query 32-block][key 64-tile][64 lanes] u32 words (attn_mask_word):
+// lane (G, c) holds (query 32*q32 + 16*gq + c, key 64*t + 16*mt + 4G + R) at
+// bit 8R + 4gq + mt.  1 bit per (query, key).
 extern "C" size_t smer_attn_drop_mask_bytes(int B, int H, int Lq, int Lk) {
-  return (size_t)B * H * ((Lq + 15) / 16) * ((Lk + 63) / 64) * 128;
+  return (size_t)B * H * ((Lq + 31) / 32) * ((Lk + 63) / 64) * 256;
 }
 
 extern "C" int smer_attn_drop_mask_gen(int B, int H, int Lq, int Lk, float drop_p, uint32_t seed,
                                        void* mask, smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && mask, "smer_attn_drop_mask_gen: bad arguments");
+  SMER_REQUIRE((((uintptr_t)mask) & 15) == 0, "smer_attn_drop_mask_gen: mask alignment");
   SMER_REQUIRE(drop_p > 0.f && drop_p < 1.f, "smer_attn_drop_mask_gen: drop_p");
-  const int nq16 = (Lq + 15) / 16, nkt = (Lk + 63) / 64;
-  const long nwords = (long)B * H * nq16 * nkt * 64;
-  hipLaunchKernelGGL(attn_drop_mask_gen_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, nwords, Lq, nq16, nkt, smer_attn_thr7(drop_p), seed,
-                     (uint16_t*)mask);
+  mask_gen_launch(B, H, Lq, Lk, smer_attn_thr7(drop_p), seed, mask, (hipStream_t)stream);
   SMER_CHECK_LAUNCH("smer_attn_drop_mask_gen");
   return SMER_OK;
 }
@@ -1803,7 +1844,7 @@ extern "C" int smer_attn_fwd_fp8(int B, int H, int Lq, int Lk, int D, const void
                                  const float* qs, unsigned* amax, smer_stream_t stream) {
   SMER_REQUIRE(o8 && qs && amax && (((uintptr_t)o8) & 3) == 0 && ldo8 % 4 == 0,
                "smer_attn_fwd_fp8: 4-B aligned copy, scale and amax");
-  SMER_REQUIRE(D == 64 && !drop_mask_in, "smer_attn_fwd_fp8: head dim 64, keep bits hashed in the kernel");
+  SMER_REQUIRE(D == 64, "smer_attn_fwd_fp8: head dim 64");
   const AttnQ8 q8{(uint8_t*)o8, ldo8, nullptr, 0, nullptr, 0, qs, amax};
   return attn_fwd_impl(SMER_BF16, B, H, Lq, Lk, D, q, ldq, k, ldk, v, ldv, o, ldo, lse, kpm, causal,
                        scale, drop_p, seed, drop_mask, drop_mask_in, q8, stream);

@@ -603,14 +603,23 @@ def test_attention_dropout(dtype, B, H, L, causal):
                    causal=causal, scale=scale, drop_p=p, seed=seed, drop_mask=mask)
         torch.cuda.synchronize()
         assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
-        # forward reading keep bits from the full-occupancy generator ==
-        # forward hashing them itself (same words, same outputs bit for bit)
+        # forward reading keep bits the caller generated beforehand ==
+        # forward with a mask buffer it fills itself == forward hashing them
+        # in its loop (no buffer): same keep decisions, outputs bit for bit
         mask3 = O.attn_drop_mask(B, H, L, L, dev)
         O.attn_drop_mask_gen(mask3, B=B, H=H, Lq=L, Lk=L, drop_p=p, seed=seed)
         o3 = torch.empty_like(o)
         lse3 = torch.empty_like(lse)
         O.attn_fwd(q, k, v, o3, lse3, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal,
                    scale=scale, drop_p=p, seed=seed, drop_mask=mask3, drop_mask_in=True)
+        o4 = torch.empty_like(o)
+        lse4 = torch.empty_like(lse)
+        O.attn_fwd(q, k, v, o4, lse4, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, causal=causal,
+                   scale=scale, drop_p=p, seed=seed)
+        torch.cuda.synchronize()
+        if not causal:  # (a causal forward skips the tiles past the diagonal)
+            assert torch.equal(mask3, mask)
+        assert torch.equal(o4, o) and torch.equal(lse4, lse)
         dq3, dk3, dv3 = torch.empty_like(dq), torch.empty_like(dk), torch.empty_like(dv)
         O.attn_bwd(q, k, v, o3, do, lse3, dq3, dk3, dv3, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm,
                    causal=causal, scale=scale, drop_p=p, seed=seed, drop_mask=mask3)
@@ -822,9 +831,10 @@ def test_adam_and_cast_and_colsum():
 @pytest.mark.parametrize("B,H,Lq,Lk,causal", [(2, 2, 96, 96, True), (2, 2, 80, 150, False),
                                               (16, 8, 512, 512, False)])
 def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
-    """The forward's stored keep bits equal tests/hashref.attn_keep_mask:
-    16-bit words [bh][q16][key tile t][lane = 16g + c], bit 4r + mt = (query
-    16*q16 + c, key 64t + 16mt + 4g + r)."""
+    """The keep bits a forward with a mask buffer leaves for the backward
+    (generated by attn_drop_mask_gen_kernel) equal tests/hashref.
+    attn_keep_mask: u32 words [bh][q32][key tile t][lane = 16G + c], bit
+    8R + 4gq + mt = (query 32*q32 + 16*gq + c, key 64t + 16mt + 4G + R)."""
     O = ops()
     D, p, seed = 64, 0.1, 99
     q, k, v, _ = _attn_inputs(B, H, Lq, Lk, D, torch.bfloat16, False)
@@ -835,11 +845,11 @@ def test_attention_drop_mask_layout(B, H, Lq, Lk, causal):
     O.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=0.125,
                drop_p=p, seed=seed, drop_mask=mask)
     torch.cuda.synchronize()
-    nq, nt = (Lq + 15) // 16, (Lk + 63) // 64
-    w = mask[: B * H * nq * nt * 128].cpu().numpy().view(np.uint16).reshape(B * H, nq, nt, 4, 16)
-    bits = (w[..., None].astype(np.uint32) >> np.arange(16, dtype=np.uint32)) & 1  # [bh,q16,t,g,c,16]
-    bits = bits.reshape(B * H, nq, nt, 4, 16, 4, 4)                                  # [.., g, c, r, mt]
-    got = bits.transpose(0, 1, 4, 2, 6, 3, 5).reshape(B * H, nq * 16, nt * 64)       # [bh, q, key]
+    nq, nt = (Lq + 31) // 32, (Lk + 63) // 64
+    w = mask[: B * H * nq * nt * 256].cpu().numpy().view(np.uint32).reshape(B * H, nq, nt, 4, 16)
+    bits = (w[..., None] >> np.arange(32, dtype=np.uint32)) & 1          # [bh, q32, t, G, c, 32]
+    bits = bits.reshape(B * H, nq, nt, 4, 16, 4, 2, 4)                   # [.., G, c, R, gq, mt]
+    got = bits.transpose(0, 1, 6, 4, 2, 7, 3, 5).reshape(B * H, nq * 32, nt * 64)  # [bh, q, key]
     ref = attn_keep_mask(seed, p, B * H * Lq, Lk).reshape(B * H, Lq, Lk)
     sel = np.ones((Lq, Lk), bool) if not causal else np.tril(np.ones((Lq, Lk), bool))
     g = got[:, :Lq, :Lk].astype(bool)

@@ -95,7 +95,11 @@ def bench_attn(cfg="c2"):
         t = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D,
                                         causal=causal, scale=sc))
         msk = ops.attn_drop_mask(B, H, Lq, Lk, dev)
+        tg = timeit(lambda: ops.attn_drop_mask_gen(msk, B=B, H=H, Lq=Lq, Lk=Lk, drop_p=0.1, seed=1))
         td = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D,
+                                         causal=causal, scale=sc, drop_p=0.1, seed=1,
+                                         drop_mask=msk, drop_mask_in=True))
+        th = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D,
                                          causal=causal, scale=sc, drop_p=0.1, seed=1,
                                          drop_mask=msk))
         do = torch.randn_like(o)
@@ -107,8 +111,9 @@ def bench_attn(cfg="c2"):
                                           B=B, H=H, Lq=Lq, Lk=Lk, D=D, causal=causal, scale=sc,
                                           drop_p=0.1, seed=1, drop_mask=msk))
         fl = 4.0 * B * H * Lq * Lk * D * (0.5 if causal else 1.0)
-        print("%-9s fwd %8.1f us %6.1f TF | fwd+drop %8.1f us | bwd %8.1f us %6.1f TF (2.5x fwd flops)"
-              " | bwd+drop %8.1f us" % (name, t, fl / t / 1e6, td, tb, 2.5 * fl / tb / 1e6, tbd))
+        print("%-9s fwd %7.1f us %6.1f TF | mask gen %6.1f | fwd+drop gen'd %7.1f (product: own %7.1f) | bwd %7.1f us "
+              "%6.1f TF (2.5x fwd flops) | bwd+drop %7.1f us"
+              % (name, t, fl / t / 1e6, tg, td, th, tb, 2.5 * fl / tb / 1e6, tbd))
 
 
 if __name__ == "__main__":
