@@ -475,24 +475,3 @@ def test_session_graph_after_pe_extension_matches_fresh(golden_dir, precision):
     for a, b in zip(first, again):
         assert np.array_equal(a, b)
 
-
-def test_fp32_decode_wide_model_unfused_matches_full_forward():
-    """ADVICE r4 (low): the fused fp32 decode layers need d_model <= 2048;
-    a wider model takes the unfused fp32 step, which still equals the full
-    recompute forward."""
-    from smer_music_generation_amd.decode import DecodeSession
-    from smer_music_generation_amd.generation import model_generate
-    from smer_music_generation_amd.model import ScoreTransformer
-    torch.manual_seed(3)
-    d, H = 2112, 33
-    m = ScoreTransformer(309, d, H, 1, 1, 256, 256, 0.0, 0.0, precision="fp32").to(dev).eval()
-    rng = np.random.default_rng(1)
-    src = rng.integers(4, 300, 24)
-    toks = rng.integers(4, 300, 6).tolist()
-    with torch.no_grad():
-        s = DecodeSession(m, 1, 24, 16)
-        s.prefill([0], [src])
-        for t in range(6):
-            got = s.step([(0, toks[t:t + 1], t)])[0]
-        full = model_generate(m, torch.from_numpy(src), toks, dev).numpy()[-1]
-    assert np.abs(got - full).max() < 1e-3
