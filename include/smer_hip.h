@@ -33,6 +33,10 @@
  *                        state -> mask -> argmax -> commit -> next feed
  *                        (generation.py:528-687 with weighted_sampling as
  *                        argmax; replaces the per-token host round trip)
+ *   smer_grammar_sample_step  the sampled (default, weighted_sampling)
+ *                        grammar loop on device: float64 softmax, sort, cdf
+ *                        search and redraws on the numpy MT19937 stream
+ *                        (generation.py:33-95, 528-687)
  *   smer_layernorm_*     residual LayerNorm, eps 1e-5 (transformer.py:392,395,
  *                        462,466,469; final norms 274-275, 329-330)
  *   smer_embed_*         embedding gather x sqrt(d) + sinusoidal PE + dropout
@@ -274,6 +278,27 @@ int smer_grammar_greedy_step_ring(int R, int V, const float* logits, long ldl, i
                                   int trash_pos, int max_span, const int32_t* src_len,
                                   int64_t* ids, int32_t* meta, int32_t* out_tok, int cap,
                                   int32_t* ctl, int32_t* ring, int ring_n, smer_stream_t stream);
+/* One sampled grammar step for R requests, drawn in request order as the
+ * host loop does (generation.py:33-95 weighted_sampling + sampling, 528-687
+ * the span loop with its redraws): e = exp(where(keep, f64(logit), -100)),
+ * p = e / np.sum(e) (numpy's pairwise order), p /= sequential sum, sort
+ * descending (ties: descending index), cdf = sequential cumsum / cdf[-1],
+ * u = numpy legacy random_sample from mt (uint32 [625]: the 624 MT19937 key
+ * words and the position, np.random.get_state() layout; updated in place),
+ * id = first cdf > u; while reject[state][id] redraw, at most 11 times.
+ * Arguments as smer_grammar_greedy_step; reject: uint8 [13, V] (the
+ * redraw checks of generation.py:556-615); out_tok ids carry bit 16 when
+ * the redraw loop gave up (the reference logs it).  state[r][8] bit 1: the
+ * row's probabilities did not sum to 1 within 1e-9 (np.random.choice's
+ * territory: the caller redoes the call on the host).  ring != NULL: ctl
+ * int32 [3] (ctl[2] = step) and the live count goes to ring[step % ring_n]
+ * (pinned host memory); else it is written to ctl[0].  V <= 512. */
+int smer_grammar_sample_step(int R, int V, const float* logits, long ldl, int32_t* state, int nst,
+                             const int8_t* targets, int max_masks, const uint8_t* keep,
+                             const uint8_t* reject, const uint8_t* cls, int eos, int m0,
+                             int trash_pos, int max_span, const int32_t* src_len, int64_t* ids,
+                             int32_t* meta, int32_t* out_tok, int cap, uint32_t* mt, int32_t* ctl,
+                             int32_t* ring, int ring_n, smer_stream_t stream);
 
 int smer_layernorm_fwd(int dtype, int M, int N, const void* x, long ldx,
                        const float* gamma, const float* beta, float eps,

@@ -88,6 +88,9 @@ SIGNATURES = {
     "smer_grammar_greedy_step_ring": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P,
                                               c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P,
                                               c_int, P]),
+    "smer_grammar_sample_step": (c_int, [c_int, c_int, P, c_long, P, c_int, P, c_int, P, P, P,
+                                         c_int, c_int, c_int, c_int, P, P, P, P, c_int, P, P, P,
+                                         c_int, P]),
     "smer_layernorm_fwd": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P,
                                    P, P]),
     "smer_layernorm_bwd_workspace": (c_size, [c_int, c_int]),

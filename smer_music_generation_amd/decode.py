@@ -427,7 +427,8 @@ class DecodeSession:
     # ------------------------------------------------------------------
     N_STATE = 12
 
-    def _capture_greedy(self, st, tg, keep, cls, cap, nm, eos, m0, lookahead, max_span, use_ring):
+    def _capture_greedy(self, st, tg, keep, cls, cap, nm, eos, m0, lookahead, max_span, use_ring,
+                        sample=False):
         """Persistent grammar buffers + the captured (decoder step + grammar)
         graph, reused by later greedy_decode calls of the same shapes."""
         dev = self.dev
@@ -447,6 +448,11 @@ class DecodeSession:
                      ring=ring if use_ring else None)
 
         def grammar():
+            if sample:
+                ops.grammar_sample_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
+                                        self.g_reject, self.g_cls, self.g_srclen, self.ids_t,
+                                        self.meta_t, self.g_out, self.g_mt, self.g_alive, **gargs)
+                return
             ops.grammar_greedy_step(self.logits_t, self.g_state, self.g_targets, self.g_keep,
                                     self.g_cls, self.g_srclen, self.ids_t, self.meta_t, self.g_out,
                                     self.g_alive, **gargs)
@@ -466,7 +472,34 @@ class DecodeSession:
         t_c = time.perf_counter()
         return g, ring, rv, t_a, t_b, t_c
 
+    def sampled_decode(self, spans, keep, reject, cls, *, eos, m0, lookahead=3, max_span=100):
+        """The sampled infill loop (the reference's default weighted_sampling
+        with its redraws) on device: each step is one replay of the captured
+        decoder step + csrc/decode_ops.hip grammar_sample_kernel, which draws
+        from numpy's global MT19937 stream -- its state is handed to the
+        device here and handed back to np.random afterwards, so the host
+        stream continues exactly as if the host had drawn.  Returns
+        (per-request emitted ids, steps, error flags, per-request redraw
+        failure flags)."""
+        st0 = np.random.get_state()
+        if st0[0] != "MT19937":
+            raise RuntimeError("sampled_decode: np.random is not MT19937")
+        mt_h = np.empty(625, dtype=np.uint32)
+        mt_h[:624] = st0[1]
+        mt_h[624] = int(st0[2])
+        res = self._grammar_decode(spans, keep, cls, eos=eos, m0=m0, lookahead=lookahead,
+                                   max_span=max_span, sample=(reject, mt_h))
+        m = self.g_mt.cpu().numpy().view(np.uint32)
+        np.random.set_state(("MT19937", m[:624].copy(), int(m[624]), st0[3], st0[4]))
+        ids, steps, err, step_ms = res
+        fails = [[(x >> 16) & 1 for x in q] for q in ids]
+        return [[x & 0xFFFF for x in q] for q in ids], steps, err, fails
+
     def greedy_decode(self, spans, keep, cls, *, eos, m0, lookahead=3, max_span=100):
+        return self._grammar_decode(spans, keep, cls, eos=eos, m0=m0, lookahead=lookahead,
+                                    max_span=max_span)
+
+    def _grammar_decode(self, spans, keep, cls, *, eos, m0, lookahead=3, max_span=100, sample=None):
         """Run the greedy infill loop of `spans` (generation._Span, one per
         request slot 0..len-1, freshly started, sources prefilled) entirely
         on device: each step is one replay of the captured decoder step +
@@ -478,7 +511,14 @@ class DecodeSession:
             raise ValueError("more spans than session slots")
         self._pe_guard()
         dev = self.dev
-        nm = max(1, max(s.n_masks for s in spans))
+        # mask-target table capacity: a power of two >= 16, so calls whose
+        # requests have different mask counts replay the same captured graph
+        # (a capture costs ~10 ms; the kernels read the table by its row
+        # stride, which is the capacity)
+        need = max(1, max(s.n_masks for s in spans))
+        nm = 16
+        while nm < need:
+            nm *= 2
         cap = self.Tmax
         st = np.zeros((self.R, self.N_STATE), dtype=np.int32)
         tg = np.zeros((self.R, nm), dtype=np.int8)
@@ -497,9 +537,18 @@ class DecodeSession:
         st[R:, 5] = 1
         if not feeds:
             return [[] for _ in range(R)], 0, np.zeros(R, dtype=np.int32), []
-        use_ring = os.environ.get("SMER_GRAMMAR_RING", "1") != "0"
-        gkey = (nm, int(max_span), int(eos), int(m0), int(lookahead), use_ring, keep.shape, cls.shape)
+        use_ring = os.environ.get("SMER_GRAMMAR_RING", "1") != "0" or sample is not None
+        gkey = (nm, int(max_span), int(eos), int(m0), int(lookahead), use_ring, keep.shape, cls.shape,
+                sample is not None)
         gc = getattr(self, "_greedy", None)
+        if sample is not None:
+            reject_t = torch.from_numpy(np.ascontiguousarray(sample[0], dtype=np.uint8))
+            mt_t = torch.from_numpy(sample[1].view(np.int32))
+            if getattr(self, "g_mt", None) is None:
+                self.g_mt = torch.zeros(625, dtype=torch.int32, device=dev)
+                self.g_reject = torch.zeros(keep.shape, dtype=torch.uint8, device=dev)
+            self.g_mt.copy_(mt_t)
+            self.g_reject.copy_(reject_t)
         if gc is not None and gc["key"] == gkey:
             # the captured step + grammar graph of an earlier call with the
             # same shapes: refresh its persistent inputs in place and replay
@@ -519,7 +568,8 @@ class DecodeSession:
             t_c = time.perf_counter()
         else:
             g, ring, rv, t_a, t_b, t_c = self._capture_greedy(st, tg, keep, cls, cap, nm, eos, m0,
-                                                             lookahead, max_span, use_ring)
+                                                             lookahead, max_span, use_ring,
+                                                             sample is not None)
             self._greedy = {"key": gkey, "graph": g, "ring": ring}
         self._load_feeds(feeds)
         max_steps = max([s.n_masks for s in spans] + [0]) * (max_span + 1) + 2

@@ -424,7 +424,7 @@ class _Precision:
 
 def generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
                    bars_to_generate, *, greedy=False, use_kv_cache=True, stats=None,
-                   precision="fp32", warm=True):
+                   precision="fp32", warm=True, device_grammar=True):
     """`generation.py:468-696`.  Returns (restored '<U9' tokens,
     mask_track_names, mask_bar_names) or None (nothing masked / on error,
     after printing it, as the reference does).  `stats` (a dict, opt-in)
@@ -437,15 +437,63 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
     sampled ids are the same draws of the same numpy stream) whatever
     precision the model trains in; None decodes at the model's own precision
     (bf16 for a default-constructed model: faster, ids may differ at
-    near-ties); the batched serving API `generation_batch` keeps None."""
+    near-ties); the batched serving API `generation_batch` keeps None.
+    device_grammar: (KV-cached path) run the grammar and the draws on the
+    device inside the captured decode step -- greedy argmax, or the default
+    weighted sampling on numpy's MT19937 stream handed to the device and back
+    (csrc/decode_ops.hip grammar_sample_kernel) -- with no host round trip
+    per token; False keeps the per-token host loop."""
     with _Precision(model, precision):
         return _generation_all(model, events, device, vocab, logger, all_controls,
                                tracks_to_generate, bars_to_generate, greedy, use_kv_cache, stats,
-                               warm)
+                               warm, device_grammar)
+
+
+_REJECT_CACHE = {}
+
+
+def reject_table(vocab):
+    """uint8 [13, V]: the redraw checks of the grammar states
+    (generation.py:556-615; grammar_spec's check), 1 = redraw."""
+    hit = _REJECT_CACHE.get(id(vocab))
+    if hit is not None and hit[0] is vocab:
+        return hit[1]
+    V = vocab.vocab_size
+    rej = np.zeros((N_GRAMMAR_STATES, V), dtype=np.uint8)
+    for c in range(N_GRAMMAR_STATES):
+        chk = grammar_spec(vocab, c)[1]
+        if chk is not None:
+            rej[c] = [bool(chk(i)) for i in range(V)]
+    _REJECT_CACHE[id(vocab)] = (vocab, rej)
+    return rej
+
+
+def _sampled_on_device(sess, st, vocab, all_controls, logger):
+    """One request's sampled span loop on device (DecodeSession.
+    sampled_decode), then the emitted ids replayed through the host span
+    (event lists, the redraw-failure log lines).  Returns the steps, or None
+    when a row's probabilities missed 1 by more than 1e-9 (np.random.choice
+    territory): the RNG is then rewound and the caller decodes on the host."""
+    keep, cls = grammar_tables(vocab, all_controls)
+    rng0 = np.random.get_state()
+    seqs, steps, err, fails = sess.sampled_decode([st], keep, reject_table(vocab), cls,
+                                                  eos=vocab.eos_index, m0=vocab.char2index('m_0'))
+    if err[0] & 2:
+        np.random.set_state(rng0)
+        return None
+    if err[0] & 1:
+        raise ValueError("decoder prefix exceeds session max_tgt %d" % (sess.Tmax - 1))
+    for idx, fail in zip(seqs[0], fails[0]):
+        if fail and logger is not None:
+            logger.info(st.spec()[2])
+        st.commit(idx)
+    if not st.done:
+        raise RuntimeError("device grammar and host replay disagree")
+    return len(seqs[0])
 
 
 def _generation_all(model, events, device, vocab, logger, all_controls, tracks_to_generate,
-                    bars_to_generate, greedy, use_kv_cache, stats, warm=True):
+                    bars_to_generate, greedy, use_kv_cache, stats, warm=True, device_grammar=True):
     try:
         src, mtn, mbn, target, no_whole = _prepare(events, vocab, tracks_to_generate,
                                                    bars_to_generate)
@@ -462,6 +510,13 @@ def _generation_all(model, events, device, vocab, logger, all_controls, tracks_t
                 sess = _batch_session(model, 1, len(src), max(128, 100 * st.n_masks + 8), None,
                                       warm=warm)
                 sess.prefill([0], [src])
+                if device_grammar and not greedy and vocab.vocab_size <= 512:
+                    n = _sampled_on_device(sess, st, vocab, all_controls, logger)
+                    if n is not None:
+                        steps = n
+                    else:  # fresh span, same RNG start: the host loop below
+                        st = _Span(vocab, src, target, all_controls, no_whole, greedy, logger)
+                        sess.prefill([0], [src])
                 fed = 0
                 while not st.done:
                     pre = st.prefix()
@@ -517,6 +572,14 @@ def _batch_session(model, R, Smax, Tmax, precision, exact_tmax=False, warm=True)
         model.set_precision(precision)
     if not warm:
         return DecodeSession(model, R, Smax, Tmax)
+    if R == 1 and not exact_tmax:
+        # the plugin call: capacities rounded up to powers of two (>= 128), so
+        # consecutive calls on sources / mask counts of similar size reuse one
+        # session and its captured graphs instead of rebuilding them (a
+        # rebuild + capture costs ~6 ms, 1/4 of a typical call); a fresh
+        # session for the same request rounds the same way
+        Smax = 1 << max(7, (int(Smax) - 1).bit_length())
+        Tmax = (1 << max(7, int(Tmax).bit_length())) - 1
     key = (id(model), model.precision, R)
     s = _BATCH_SESSIONS.get(key)
     fits = (s is not None and s.model is model and s.Smax >= Smax and s.Tmax >= Tmax + 1

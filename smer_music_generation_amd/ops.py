@@ -503,6 +503,33 @@ def grammar_greedy_step(logits, state, targets, keep, cls, src_len, ids, meta, o
          _p(src_len), _p(ids), _p(meta), _p(out_tok), out_tok.shape[1], _p(alive), _stream())
 
 
+def grammar_sample_step(logits, state, targets, keep, reject, cls, src_len, ids, meta, out_tok, mt,
+                        ctl, *, eos, m0, trash_pos, max_span=100, ring=None):
+    """The sampled grammar step (smer_grammar_sample_step): mt uint32 [625]
+    (numpy MT19937 key + position, updated in place), ctl int32 [3]; with
+    `ring` (pinned host int32 [n]) the live count lands in ring[step % n],
+    else in ctl[0]."""
+    R, nst = state.shape
+    V = keep.shape[1]
+    for t, dt in ((state, torch.int32), (targets, torch.int8), (keep, torch.uint8),
+                  (reject, torch.uint8), (cls, torch.uint8), (src_len, torch.int32),
+                  (ids, torch.int64), (meta, torch.int32), (out_tok, torch.int32),
+                  (mt, torch.int32), (ctl, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise RuntimeError("grammar_sample_step: expected contiguous %s" % dt)
+    if logits.shape[0] < 2 * R or ids.shape[0] != 2 * R or meta.shape != (4, 2 * R) or \
+            targets.shape[0] != R or keep.shape[0] != 13 or reject.shape != keep.shape or \
+            cls.shape[0] != V or src_len.shape[0] != R or mt.numel() < 625 or ctl.numel() < 3:
+        raise RuntimeError("grammar_sample_step: shape mismatch")
+    if ring is not None and (ring.dtype != torch.int32 or not ring.is_pinned()):
+        raise RuntimeError("grammar_sample_step: ring must be pinned int32")
+    call("smer_grammar_sample_step", R, V, _p(logits), _ld(logits), _p(state), nst, _p(targets),
+         targets.shape[1], _p(keep), _p(reject), _p(cls), int(eos), int(m0), int(trash_pos),
+         int(max_span), _p(src_len), _p(ids), _p(meta), _p(out_tok), out_tok.shape[1], _p(mt),
+         _p(ctl), ring.data_ptr() if ring is not None else None, ring.numel() if ring is not None else 0,
+         _stream())
+
+
 # ---------------------------------------------------------------------------
 def layernorm(x, gamma, beta, y, mean, rstd, eps=1e-5):
     M, N = x.shape

@@ -66,3 +66,19 @@ def test_choice1_rejects_like_numpy():
             np.random.choice(a, size=1, p=p)
         with pytest.raises(ValueError):
             G._choice1(a, p)
+
+
+def test_reject_table_matches_grammar_checks():
+    """The device sampler's redraw table (generation.reject_table) holds the
+    reference's redraw checks (generation.py:556-615, grammar_spec) state by
+    state: 1 exactly where the check asks for another draw."""
+    from smer_music_generation_amd.generation import N_GRAMMAR_STATES, grammar_spec, reject_table
+    from smer_music_generation_amd.vocab import WordVocab
+    v = WordVocab(0, ['key', 'tensile', 'density', 'polyphony', 'occupation'])
+    rej = reject_table(v)
+    assert rej.shape == (N_GRAMMAR_STATES, v.vocab_size)
+    for code in range(N_GRAMMAR_STATES):
+        chk = grammar_spec(v, code)[1]
+        want = [bool(chk(i)) if chk is not None else False for i in range(v.vocab_size)]
+        assert [bool(x) for x in rej[code]] == want
+    assert rej[0].sum() > 0 and rej[6:10].sum() == 0 and rej[11:].sum() == 0
