@@ -110,12 +110,13 @@ int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long ld
                          float* db, int db_accumulate, void* workspace, size_t ws_bytes,
                          smer_stream_t stream);
 
-/* Diagnostics: when buf (device, >= 64 * num_CUs uint64) is non-NULL, the
+/* Diagnostics: when buf (device, bytes >= 64 * num_CUs uint64) is non-NULL, the
  * staggered 256x256 GEMM (the forward / dgrad shapes of transformer.py:389-395,
  * 459-469) writes per wave s_memtime stamps of its first two tiles (tile
  * start, k-loop start, k-loop end, epilogue end) at buf[(block * 8 + wave) * 8
- * + k].  NULL (the default) turns them off.  Used by tools/gemm256s_phases.py. */
-int smer_gemm_debug_stamps(void* buf);
+ * + k].  NULL (the default) turns them off; launches on a capturing stream
+ * never stamp.  Used by tools/gemm256s_phases.py. */
+int smer_gemm_debug_stamps(void* buf, size_t bytes);
 
 /* Flash attention over [B*L, *] token-row layouts (row = b*L + i), head h
  * at column h*D.  kpm: uint8 [B, Lk] (1 = padded key) or NULL.  causal:

@@ -1309,11 +1309,26 @@ __global__ __launch_bounds__(512, 1) void gemm256s_bf16_kernel(int M, int N, int
   }
 }
 
+static int smer_num_cus();
 // phase stamps of the staggered kernel (diagnostics; tools/gemm256s_phases.py)
 static unsigned long long* g_gemm_dbg = nullptr;
-extern "C" int smer_gemm_debug_stamps(void* buf) {
+static size_t g_gemm_dbg_bytes = 0;
+extern "C" int smer_gemm_debug_stamps(void* buf, size_t bytes) {
+  SMER_REQUIRE(!buf || bytes >= (size_t)64 * smer_num_cus() * sizeof(unsigned long long),
+               "smer_gemm_debug_stamps: the buffer holds 64 stamps per CU");
   g_gemm_dbg = (unsigned long long*)buf;
+  g_gemm_dbg_bytes = buf ? bytes : 0;
   return SMER_OK;
+}
+// the stamp buffer for a launch of `grid` workgroups on stream s: none while
+// the stream is capturing (a graph would keep the pointer past the tool's
+// buffer) or when the buffer is too small for the grid
+static unsigned long long* gemm_dbg_for(int grid, hipStream_t s) {
+  if (!g_gemm_dbg) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if ((size_t)grid * 64 * sizeof(unsigned long long) > g_gemm_dbg_bytes) return nullptr;
+  return g_gemm_dbg;
 }
 
 // ---------------------------------------------------------------------------
@@ -2160,7 +2175,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       }
       const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
       GemmEpi ed = e;
-      ed.dbg = g_gemm_dbg;
+      ed.dbg = gemm_dbg_for(grid, s);
       hipLaunchKernelGGL(gemm256s_bf16_kernel<BKC>, dim3(grid), dim3(512), G2_LDS, s,
                          M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, ed);
       return;

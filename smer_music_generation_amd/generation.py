@@ -431,7 +431,9 @@ def generation_all(model, events, device, vocab, logger, all_controls, tracks_to
     receives the number of decode steps (= tokens drawn).
     warm: decode on this model's cached batch-1 session (KV caches and the
     captured step graph kept across calls, as in generation_batch); False
-    builds a private session freed after the call.
+    builds a private session freed after the call.  A warm session is not
+    re-entrant: concurrent calls on one model (threads) would share its
+    caches and graph, so serialise them or pass warm=False.
     precision: arithmetic of this call's decode.  "fp32" (default) gives
     the reference's token ids bit for bit (north_star: bit-exact greedy ids;
     sampled ids are the same draws of the same numpy stream) whatever

@@ -48,10 +48,10 @@ def main():
             ops.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)
         torch.cuda.synchronize()
         buf.zero_()
-        lib.smer_gemm_debug_stamps(ctypes.c_void_p(buf.data_ptr()))
+        lib.smer_gemm_debug_stamps(ctypes.c_void_p(buf.data_ptr()), buf.numel() * buf.element_size())
         ops.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)
         torch.cuda.synchronize()
-        lib.smer_gemm_debug_stamps(ctypes.c_void_p(0))
+        lib.smer_gemm_debug_stamps(ctypes.c_void_p(0), 0)
         st = buf[:256 * 64].view(256, 8, 8).cpu().numpy().astype(np.float64)
         nk = K // 32
         for tile in (0, 1):
