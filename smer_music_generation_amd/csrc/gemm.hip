@@ -2088,16 +2088,17 @@ static long smer_skinny16_cap() {  // workgroups per CU (SMER_SKINNY16_CAP; A/B 
   return v;
 }
 
-// Resident split-K workgroups per 2 CUs (SMER_WGRAD_WGP2: 4 = two per CU,
-// the default; 2 = one per CU; 1 = one per two CUs).  The weight gradients
-// run on a second stream beside the main chain: a smaller persistent grid
-// leaves CUs (and LDS) to the main stream's kernels and cuts the split-K
-// slab bytes in proportion.
+// Resident split-K workgroups per 2 CUs (SMER_WGRAD_WGP2: 4 = two per CU;
+// 2 = one per CU, the default since round 5: C2 13.49 vs 13.56 ms, C4 fp8
+// 86.84 vs 87.05 ms, three / two interleaved rounds of tools/ab_step.py;
+// 1 = one per two CUs).  The weight gradients run on a second stream beside
+// the main chain: a smaller persistent grid leaves CUs (and LDS) to the main
+// stream's kernels and cuts the split-K slab bytes in proportion.
 static long smer_wgrad_resident() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD_WGP2");
-    v = e ? std::max(1, std::min(4, atoi(e))) : 4;
+    v = e ? std::max(1, std::min(4, atoi(e))) : 2;
   }
   return std::max(8L, (v * (long)smer_num_cus()) / 2);
 }

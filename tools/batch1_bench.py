@@ -106,3 +106,52 @@ def breakdown():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "breakdown":
     breakdown()
+
+
+def lookahead_sweep():
+    """The batch-1 plugin line with the device loop's lookahead (graph
+    replays in flight ahead of the host's poll) at 1, 2 and 3."""
+    from smer_music_generation_amd import decode
+    f = decode.DecodeSession.sampled_decode
+    args = bench.parse_args([])
+    dev = torch.device("cuda:0")
+    res = {}
+    for la in (3, 1, 3, 1, 3, 1, 2):
+        def g(self, *a, _la=la, **k):
+            k["lookahead"] = _la
+            return f(self, *a, **k)
+        decode.DecodeSession.sampled_decode = g
+        r = bench.bench_infill_batch1(args, dev, 0)
+        res.setdefault(str(la), []).append((r["value"], r["warm_call_s_mean"]))
+    decode.DecodeSession.sampled_decode = f
+    print(json.dumps(res))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lookahead":
+    lookahead_sweep()
+
+
+def env_sweep(name, values, rounds=2):
+    """The batch-1 plugin line with a per-process switch: each value in its
+    own child process (switches are read once per process), interleaved."""
+    import subprocess
+    res = {v: [] for v in values}
+    for _ in range(rounds):
+        for v in values:
+            env = dict(os.environ)
+            env[name] = v
+            out = subprocess.run([sys.executable, os.path.abspath(__file__), "one"], env=env,
+                                 capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(out.stdout[-2000:], out.stderr[-2000:])
+                sys.exit(out.returncode)
+            res[v].append(json.loads(out.stdout.strip().splitlines()[-1])["value"])
+            print(name, v, res[v][-1], flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "one":
+    print(json.dumps(bench.bench_infill_batch1(bench.parse_args([]), torch.device("cuda:0"), 0)))
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "env":
+    env_sweep(sys.argv[2], sys.argv[3:])
