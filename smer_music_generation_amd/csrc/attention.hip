@@ -2030,7 +2030,12 @@ extern "C" int smer_attn_decode_split_f32(int n_rows, int H, int D, const void* 
   if (head_stride <= 0) head_stride = D;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(H, n_rows, 8);
-  hipLaunchKernelGGL((attn_decode_vec_kernel<float, 16, 2, 4, false, 0, 8>), grid, dim3(256), 0, s, (const float*)q,
+  // pipelined key loads (the next key step requested before this step's
+  // math; the same arithmetic as the unpipelined form, so the same bits):
+  // batch-1 plugin call 2,621 vs 2,534 tokens/s (two rounds,
+  // tools/batch1_bench.py env SMER_DEC_SPLIT_CFG; 8-wave and 4-step forms
+  // 2,558-2,607)
+  hipLaunchKernelGGL((attn_decode_vec_kernel<float, 16, 2, 4, true, 0, 8>), grid, dim3(256), 0, s, (const float*)q,
                      ldq, (const float*)kcache, (const float*)vcache, row_stride, req_stride, head_stride, row_req,
                      row_nkeys, (float*)nullptr, 0L, scale, DecQ{}, 0, part);
   SMER_CHECK_LAUNCH("smer_attn_decode_split_f32");

@@ -2363,13 +2363,24 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_f32_kernel(int M, int
 
 // fp32 NT GEMM on the fp32 MFMA (v_mfma_f32_16x16x4_f32: fp32 products and
 // sums): the parity-mode prefill (encoder Linears and the cross K/V of a
-// ~1k-token source: 104 us per Linear on the VALU tile kernel) and fp32
-// training forwards.  64x64 tiles, 4 waves of 32x32 (2x2 MFMA blocks); the
-// contraction of a 64-deep chunk runs in lane-group order (MFMA c sums
-// k = 16 g + c over the lane groups g), so a lane streams 16 consecutive
-// floats of one A row and one B row per block straight from global memory
-// (the 4 waves share rows through L1), next chunk requested before this
-// chunk's 64 MFMAs.
+// ~1k-token source) and fp32 training forwards.  64x64 tiles, 4 waves of
+// 32x32 (2x2 MFMA blocks); the contraction of a 64-deep chunk runs in
+// lane-group order (MFMA c sums k = 16 g + c over the lane groups g), so a
+// lane streams 16 consecutive floats of one A row and one B row per block
+// straight from global memory (the 4 waves share rows through L1).  Whole
+// chunks are loaded unconditionally (rows outside M / N read row 0 and are
+// dropped by the epilogue's bounds) into a ring of PD + 1 register buffers,
+// PD chunks ahead of the MFMAs: the guarded loads of round 4 (a select
+// behind each load) made hipcc wait for every outstanding load before each
+// chunk's MFMAs (vmcnt(0)).  A partial last chunk (K % 64) is loaded
+// guarded.  Measured (tools/gemm_f32_shapes.py, M = 1050 prefill shapes):
+// the four encoder Linears 204.5 us per layer at PD = 2 vs 222.5 guarded;
+// staging the chunks through a double-buffered LDS tile with coalesced
+// 256-B row loads (same operands, 69.6 KB of LDS: two workgroups per CU)
+// ran 248 us; a load pattern with whole rows per instruction (a timing
+// probe with the wrong operands) 147-153 us, which needs the operands
+// transposed across lanes.
+template <int PD>
 __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(int M, int N, int K, const float* __restrict__ A,
                                                             long lda, const float* __restrict__ B, long ldb,
                                                             GemmEpi e) {
@@ -2378,24 +2389,19 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(int M, int N, int K,
   const int m0 = blockIdx.y * 64 + (wave >> 1) * 32, n0 = blockIdx.x * 64 + (wave & 1) * 32;
   const float* ap[2];
   const float* bp[2];
-  bool aok[2], bok[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = m0 + 16 * i + c16, c = n0 + 16 * i + c16;
-    aok[i] = r < M;
-    bok[i] = c < N;
-    ap[i] = A + (long)(aok[i] ? r : 0) * lda + 16 * g;
-    bp[i] = B + (long)(bok[i] ? c : 0) * ldb + 16 * g;
+    ap[i] = A + (long)(r < M ? r : 0) * lda + 16 * g;
+    bp[i] = B + (long)(c < N ? c : 0) * ldb + 16 * g;
   }
   auto load = [&](int k0, float4 (&fa)[2][4], float4 (&fb)[2][4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int k = k0 + 16 * g + 4 * t;
-        const bool kok = k < K;  // K % 4 == 0: a float4 is all in or all out
-        fa[i][t] = (aok[i] && kok) ? *reinterpret_cast<const float4*>(ap[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
-        fb[i][t] = (bok[i] && kok) ? *reinterpret_cast<const float4*>(bp[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
+        fa[i][t] = *reinterpret_cast<const float4*>(ap[i] + k0 + 4 * t);
+        fb[i][t] = *reinterpret_cast<const float4*>(bp[i] + k0 + 4 * t);
       }
   };
   f32x4 acc[2][2];
@@ -2403,11 +2409,7 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(int M, int N, int K,
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 fa[2][4], fb[2][4];
-  load(0, fa, fb);
-  for (int k0 = 0; k0 < K; k0 += 64) {
-    float4 na[2][4], nb[2][4];
-    if (k0 + 64 < K) load(k0 + 64, na, nb);
+  auto mma = [&](const float4 (&fa)[2][4], const float4 (&fb)[2][4]) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -2420,12 +2422,34 @@ __global__ __launch_bounds__(256) void gemm_f32_mfma_kernel(int M, int N, int K,
             const float b = q == 0 ? fb[j][t].x : q == 1 ? fb[j][t].y : q == 2 ? fb[j][t].z : fb[j][t].w;
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
           }
-    if (k0 + 64 < K) {
+  };
+  const int nfull = K / 64;
+  if (nfull > 0) {  // block-uniform
+    float4 ra[PD + 1][2][4], rb[PD + 1][2][4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int p = 0; p < PD; ++p) load(64 * min(p, nfull - 1), ra[p], rb[p]);
+    for (int c = 0; c < nfull; c += PD + 1) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) { fa[i][t] = na[i][t]; fb[i][t] = nb[i][t]; }
+      for (int s = 0; s <= PD; ++s) {
+        // chunk c + s sits in slot s; slot s - 1 (just consumed) takes chunk
+        // c + s + PD (clamped: a redundant reload near the end)
+        load(64 * min(c + s + PD, nfull - 1), ra[(s + PD) % (PD + 1)], rb[(s + PD) % (PD + 1)]);
+        if (c + s < nfull) mma(ra[s], rb[s]);
+      }
     }
+  }
+  if (K % 64) {  // partial last chunk: K % 4 == 0, a float4 is all in or all out
+    float4 fa[2][4], fb[2][4];
+    const int k0 = nfull * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bool kok = k0 + 16 * g + 4 * t < K;
+        fa[i][t] = kok ? *reinterpret_cast<const float4*>(ap[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
+        fb[i][t] = kok ? *reinterpret_cast<const float4*>(bp[i] + k0 + 4 * t) : make_float4(0, 0, 0, 0);
+      }
+    mma(fa, fb);
   }
   // D[row 4g + r][col c16] of each block
 #pragma unroll
@@ -2456,7 +2480,7 @@ static void launch_f32(int M, int N, int K, const void* A, long lda, const void*
   dim3 grid((N + 63) / 64, (M + 63) / 64);
   if (AK && BKC && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
       (((uintptr_t)A | (uintptr_t)B) & 15) == 0 && smer_gemm_f32_mfma()) {
-    hipLaunchKernelGGL(gemm_f32_mfma_kernel, grid, dim3(256), 0, s, M, N, K, (const float*)A, lda,
+    hipLaunchKernelGGL(gemm_f32_mfma_kernel<2>, grid, dim3(256), 0, s, M, N, K, (const float*)A, lda,
                        (const float*)B, ldb, e);
     return;
   }
