@@ -174,6 +174,29 @@ __device__ __forceinline__ void load8(const T* p, int valid, float (&v)[8]) {
 // ln_fwd_kernel and the decode Linear's LayerNorm prologue so that both
 // produce the same bits.
 constexpr int LNR_MAXC = 4;
+// the statistics of a row already in v (chunks ch >= N / 8 ignored)
+template <int NC = LNR_MAXC>
+__device__ __forceinline__ void ln_stats_loaded(const float (&v)[NC][8], int N, float eps, int lane, float& mu,
+                                                float& rs) {
+  const int nch = N >> 3;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+  mu = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (lane + 64 * c < nch)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        q += d * d;
+      }
+  rs = rsqrtf(wave_sum(q) / N + eps);
+}
 template <typename T, int NC = LNR_MAXC>
 __device__ __forceinline__ void ln_row_stats(const T* __restrict__ xr, int N, float eps, int lane,
                                              float (&v)[NC][8], float& mu, float& rs) {

@@ -2467,11 +2467,26 @@ static bool smer_gemm_f32_mfma() {
   return !(e && e[0] == '0');
 }
 
+static void launch_skinny_rows_f32(int M, int N, int K, const float* A, long lda, const float* W, long ldw,
+                                   const GemmEpi& e, hipStream_t s);
+// SMER_SKINNY_ROWS_F32=0: fp32 Linears of <= 64 rows on gemm_skinny_f32_kernel (A/B runs)
+static bool smer_skinny_rows_f32() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_SKINNY_ROWS_F32");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
 template <bool AK, bool BKC>
 static void launch_f32(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                        const GemmEpi& e, hipStream_t s) {
   if (AK && BKC && M <= 64 && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
       (((uintptr_t)A | (uintptr_t)B) & 15) == 0) {
+    if (K <= SKF_NW * SKF_UNR * 64 && smer_skinny_rows_f32()) {
+      launch_skinny_rows_f32(M, N, K, (const float*)A, lda, (const float*)B, ldb, e, s);
+      return;
+    }
     const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
     hipLaunchKernelGGL(gemm_skinny_f32_kernel, grid, dim3(64 * SKF_NW), 0, s, M, N, K, (const float*)A,
                        lda, (const float*)B, ldb, e);
@@ -2734,6 +2749,14 @@ extern "C" int smer_linear_decode(int M, int N, int K, const void* A, long lda, 
 // their HBM latency overlaps the row statistics; each workgroup normalises
 // its rows into LDS with ln_row_stats / ln_apply (the fp32 LayerNorm
 // kernel's arithmetic: same bits), workgroup 0 also stores them to X.
+// LN = false (smer_linear_decode_f32 and fp32 Linears of <= 64 rows with
+// K <= 2048): the rows are copied into LDS unchanged -- the same products in
+// the same order as gemm_skinny_f32_kernel, whose row loads sat behind the
+// weight loads in one dependent chain per k step.  The weight loads are
+// unconditional (column clamped to N - 1, k to K - 4; the FMAs skip k >= K):
+// the guarded loads of round 4 left a phi copy behind the second load, so
+// every workgroup waited for it (vmcnt(0)) before requesting the rest.
+template <bool LN>
 __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, int N, int K,
                                                                          const float* __restrict__ Y, long ldy,
                                                                          const float* __restrict__ gamma,
@@ -2748,27 +2771,67 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, 
   const int cq = lane >> 4, kq = lane & 15;
   const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
   const int col = n0 + cq;
-  const bool colok = col < N;
   const int mrows = min(SKF_BM, M - m0);
-  const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  const float* bp = B + (long)min(col, N - 1) * ldb;
+  // loads in the order they are needed (vmcnt counts in order): this wave's
+  // first row (and the LayerNorm's gamma / beta), then the weights, so the
+  // row work waits for the row alone.  Chunk indices are clamped, not
+  // guarded: a clamped chunk rereads (and rewrites) the row's last one.
+  const int nch = K >> 3, n4 = K >> 2;
+  const float* y0 = Y + (long)(m0 + min(wave, mrows - 1)) * ldy;
+  float4 t[SKF_UNR];  // !LN: the first row, 16 B per lane per chunk
+  float v0[LNR_MAXC][8], gv[LNR_MAXC][8], bv[LNR_MAXC][8];  // LN: 32 B per lane per chunk
+  if constexpr (LN) {
+#pragma unroll
+    for (int c = 0; c < LNR_MAXC; ++c) {
+      const int ch = min(lane + 64 * c, nch - 1);
+      load8<float>(y0 + ch * 8, 8, v0[c]);
+      load8<float>(gamma + ch * 8, 8, gv[c]);
+      load8<float>(beta + ch * 8, 8, bv[c]);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < SKF_UNR; ++c) t[c] = *reinterpret_cast<const float4*>(y0 + 4 * min(lane + 64 * c, n4 - 1));
+  }
+  // compiler memory barrier: hipcc otherwise sinks the row loads behind the
+  // weight loads (into the row loop), and the row work then waits for both
+  asm volatile("" ::: "memory");
   float4 b[SKF_UNR];
 #pragma unroll
   for (int u = 0; u < SKF_UNR; ++u) {
-    const int k = (wave + u * SKF_NW) * 64;
-    b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
+    const int k = (wave + u * SKF_NW) * 64 + 4 * kq;
+    b[u] = *reinterpret_cast<const float4*>(bp + min(k, K - 4));
   }
-  const int nch = K >> 3;
-  for (int rr = wave; rr < mrows; rr += SKF_NW) {  // wave-uniform
+  if constexpr (!LN) {
+    for (int rr = wave; rr < mrows; rr += SKF_NW) {  // wave-uniform
+      if (rr != wave) {
+        const float* yr = Y + (long)(m0 + rr) * ldy;
+#pragma unroll
+        for (int c = 0; c < SKF_UNR; ++c) t[c] = *reinterpret_cast<const float4*>(yr + 4 * min(lane + 64 * c, n4 - 1));
+      }
+#pragma unroll
+      for (int c = 0; c < SKF_UNR; ++c) *reinterpret_cast<float4*>(xs + rr * K + 4 * min(lane + 64 * c, n4 - 1)) = t[c];
+    }
+  }
+  for (int rr = wave; LN && rr < mrows; rr += SKF_NW) {  // wave-uniform
     const int row = m0 + rr;
     float v[LNR_MAXC][8], mu, rs;
-    ln_row_stats<float>(Y + (long)row * ldy, K, eps, lane, v, mu, rs);
+    if (rr == wave) {
+#pragma unroll
+      for (int c = 0; c < LNR_MAXC; ++c)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = v0[c][i];
+      ln_stats_loaded(v, K, eps, lane, mu, rs);
+    } else {
+      ln_row_stats<float>(Y + (long)row * ldy, K, eps, lane, v, mu, rs);
+    }
 #pragma unroll
     for (int c = 0; c < LNR_MAXC; ++c) {
       const int ch = lane + 64 * c;
       if (ch < nch) {
         float o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gamma[ch * 8 + i], beta[ch * 8 + i]);
+        for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, gv[c][i], bv[c][i]);
         float* dst = xs + rr * K + ch * 8;
         *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
         *reinterpret_cast<float4*>(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
@@ -2824,6 +2887,28 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, 
   }
 }
 
+// up to 128 KiB of dynamic LDS (16 rows x 2048) for the LDS-row skinny kernels
+static void skinny_f32_lds_attr() {
+  static bool set = false;
+  if (!set) {
+    hipFuncSetAttribute((const void*)gemm_skinny_ln_f32_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        SKF_BM * 2048 * (int)sizeof(float));
+    hipFuncSetAttribute((const void*)gemm_skinny_ln_f32_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        SKF_BM * 2048 * (int)sizeof(float));
+    set = true;
+  }
+}
+// fp32 Linear of <= 64 rows, K <= 2048 (K % 4 == 0, 16-B aligned rows):
+// rows through LDS, all weight loads of the single round issued first
+static void launch_skinny_rows_f32(int M, int N, int K, const float* A, long lda, const float* W, long ldw,
+                                   const GemmEpi& e, hipStream_t s) {
+  skinny_f32_lds_attr();
+  const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+  const size_t lds = (size_t)std::min(M, SKF_BM) * K * sizeof(float);
+  hipLaunchKernelGGL(gemm_skinny_ln_f32_kernel<false>, grid, dim3(64 * SKF_NW), lds, s, M, N, K, A, lda,
+                     (const float*)nullptr, (const float*)nullptr, 0.f, (float*)nullptr, 0L, W, ldw, e);
+}
+
 // fp32 decode Linear whose input rows are the attention output merged from
 // smer_attn_decode_split_f32's per-slice partials (the cross-attention
 // out-projection of the plugin's fp32 step): the prologue merges the NS = 8
@@ -2843,14 +2928,13 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_merge_f32_kernel(int 
   const int cq = lane >> 4, kq = lane & 15;
   const int n0 = blockIdx.x * SKF_BN, m0 = blockIdx.y * SKF_BM;
   const int col = n0 + cq;
-  const bool colok = col < N;
   const int mrows = min(SKF_BM, M - m0);
-  const float* bp = B + (long)(colok ? col : 0) * ldb + 4 * kq;
+  const float* bp = B + (long)min(col, N - 1) * ldb;
   float4 b[SKF_UNR];
 #pragma unroll
-  for (int u = 0; u < SKF_UNR; ++u) {
-    const int k = (wave + u * SKF_NW) * 64;
-    b[u] = (colok && k + 4 * kq < K) ? *reinterpret_cast<const float4*>(bp + k) : make_float4(0, 0, 0, 0);
+  for (int u = 0; u < SKF_UNR; ++u) {  // unconditional (see gemm_skinny_ln_f32_kernel)
+    const int k = (wave + u * SKF_NW) * 64 + 4 * kq;
+    b[u] = *reinterpret_cast<const float4*>(bp + min(k, K - 4));
   }
   const int H = K / 64;
   for (int t = wave; t < mrows * H; t += SKF_NW) {  // wave-uniform: (row, head) records
@@ -2937,9 +3021,13 @@ extern "C" int smer_linear_decode_f32(int M, int N, int K, const void* A, long l
   SMER_REQUIRE(!kv || (kv_req && kv_pos && kv_col0 >= 0 && kv_col0 < N), "smer_linear_decode_f32: kv scatter arguments");
   const GemmEpi e = decode_epi(bias, relu, residual, ldr, C, ldc, Cf, ldcf, kv, kv_row_stride, kv_req_stride,
                                kv_req, kv_pos, kv_col0);
-  const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
-  hipLaunchKernelGGL(gemm_skinny_f32_kernel, grid, dim3(64 * SKF_NW), 0, (hipStream_t)stream, M, N, K,
-                     (const float*)A, lda, (const float*)W, ldw, e);
+  if (K <= SKF_NW * SKF_UNR * 64 && smer_skinny_rows_f32()) {
+    launch_skinny_rows_f32(M, N, K, (const float*)A, lda, (const float*)W, ldw, e, (hipStream_t)stream);
+  } else {
+    const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
+    hipLaunchKernelGGL(gemm_skinny_f32_kernel, grid, dim3(64 * SKF_NW), 0, (hipStream_t)stream, M, N, K,
+                       (const float*)A, lda, (const float*)W, ldw, e);
+  }
   SMER_CHECK_LAUNCH("smer_linear_decode_f32");
   return SMER_OK;
 }
@@ -2963,13 +3051,8 @@ extern "C" int smer_linear_decode_ln_f32(int M, int N, int K, const void* Y, lon
                                kv_req, kv_pos, kv_col0);
   const dim3 grid((N + SKF_BN - 1) / SKF_BN, (M + SKF_BM - 1) / SKF_BM);
   const size_t lds = (size_t)std::min(M, SKF_BM) * K * sizeof(float);
-  static bool attr_set = false;  // up to 128 KiB of dynamic LDS (16 rows x 2048)
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_skinny_ln_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        SKF_BM * 2048 * (int)sizeof(float));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(gemm_skinny_ln_f32_kernel, grid, dim3(64 * SKF_NW), lds, (hipStream_t)stream, M, N, K,
+  skinny_f32_lds_attr();
+  hipLaunchKernelGGL(gemm_skinny_ln_f32_kernel<true>, grid, dim3(64 * SKF_NW), lds, (hipStream_t)stream, M, N, K,
                      (const float*)Y, ldy, gamma, beta, eps, (float*)X, ldx, (const float*)W, ldw, e);
   SMER_CHECK_LAUNCH("smer_linear_decode_ln_f32");
   return SMER_OK;
