@@ -1728,25 +1728,34 @@ constexpr int SK_BM = 64, SK_BN = 16;
 // The epilogue's bias / residual for one 8-column chunk, loaded BEFORE the K
 // loop so that their HBM latency overlaps the operand loads (a decode-step
 // GEMM is a handful of dependent memory round trips; this removes one).
+// raw prefetched epilogue operands (converted at use: a conversion right
+// behind the load makes hipcc wait for it there)
 struct EpiPre {
-  float b[8];
-  float r[8];
+  float4 b0, b1;
+  bf16x8 r;
 };
 __device__ __forceinline__ bool epi_pre_ok(const GemmEpi& e, int M, int N, int row, int col) {
   return e.vec && row < M && col + 8 <= N;
 }
+// unconditional per thread (row / column clamped into the matrix; the
+// caller uses the values only where epi_pre_ok holds): requested after the
+// kernel's operand loads, a guarded form made every thread wait for it
+// before issuing them
+__device__ __forceinline__ void epi_prefetch_clamped(const GemmEpi& e, int M, int N, int row, int col, EpiPre& p) {
+  if (!e.vec || N < 8) return;  // uniform
+  const int c = min(col, N - 8), r = min(row, M - 1);
+  if (e.bias) {
+    p.b0 = *reinterpret_cast<const float4*>(e.bias + c);
+    p.b1 = *reinterpret_cast<const float4*>(e.bias + c + 4);
+  }
+  if (e.residual) p.r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)r * e.ldr + c);
+}
 __device__ __forceinline__ void epi_prefetch(const GemmEpi& e, int row, int col, EpiPre& p) {
   if (e.bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(e.bias + col);
-    const float4 b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
-    p.b[0] = b0.x; p.b[1] = b0.y; p.b[2] = b0.z; p.b[3] = b0.w;
-    p.b[4] = b1.x; p.b[5] = b1.y; p.b[6] = b1.z; p.b[7] = b1.w;
+    p.b0 = *reinterpret_cast<const float4*>(e.bias + col);
+    p.b1 = *reinterpret_cast<const float4*>(e.bias + col + 4);
   }
-  if (e.residual) {
-    const bf16x8 r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)row * e.ldr + col);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) p.r[k] = (float)r[k];
-  }
+  if (e.residual) p.r = *reinterpret_cast<const bf16x8*>((const bf16*)e.residual + (long)row * e.ldr + col);
 }
 // epi_apply8 with the prefetched bias / residual (vector path only)
 __device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int col, float (&v)[8],
@@ -1754,8 +1763,9 @@ __device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int co
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] *= e.alpha;
   if (e.bias) {
+    const float pb[8] = {p.b0.x, p.b0.y, p.b0.z, p.b0.w, p.b1.x, p.b1.y, p.b1.z, p.b1.w};
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += p.b[k];
+    for (int k = 0; k < 8; ++k) v[k] += pb[k];
   }
   if (e.relu) {
 #pragma unroll
@@ -1764,7 +1774,7 @@ __device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int co
   if (e.drop_thr) smer_drop8(smer_rowkey(e.seed, (uint32_t)row), e.drop_thr, e.drop_scale, (uint32_t)col, v);
   if (e.residual) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] += p.r[k];
+    for (int k = 0; k < 8; ++k) v[k] += (float)p.r[k];
   }
   GemmEpi e2 = e;  // the rest (gate, stores) through the shared path
   e2.alpha = 1.f; e2.bias = nullptr; e2.relu = 0; e2.drop_thr = 0; e2.residual = nullptr;
@@ -1784,7 +1794,13 @@ __device__ __forceinline__ void epi_apply8_pre(const GemmEpi& e, int row, int co
 // streams its BM rows of A and 16 rows of W over all of K, so its load time
 // grows with (BM + 16) * K: MI = 1 quarters the A bytes per workgroup of
 // the 64-row strip (4x the workgroups, each re-reading its W strip).
-template <int NW, int UNR, int MI = 4>
+// KF (K % 32 == 0): every lane's 8-chunk of a valid K step is in range, so
+// the operand loads are unconditional (rows / columns clamped into the
+// matrices -- their outputs are dropped -- and steps past K reread the last
+// step and skip their MFMAs): a guarded load (select behind it) made hipcc
+// wait for each one.  The epilogue's bias / residual are requested after the
+// operands (before: first, guarded, and waited for before any operand load).
+template <int NW, int UNR, int MI = 4, bool KF = false>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny_bf16_kernel(int M, int N, int K,
                                                                    const bf16* __restrict__ A, long lda,
                                                                    const bf16* __restrict__ B, long ldb,
@@ -1801,15 +1817,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_bf16_kernel(int M, int N,
   const bool eth = tid < BM * 2;
   const bool pre = eth && epi_pre_ok(e, M, N, erow, ecol);
   EpiPre ep;
-  if (pre) epi_prefetch(e, erow, ecol, ep);
-  const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
+  if (!KF && pre) epi_prefetch(e, erow, ecol, ep);
+  const bf16* bp = B + (long)(KF ? min(ncol, N - 1) : (colok ? ncol : 0)) * ldb + kq;
   const bf16* ap[MI];
   bool rowok[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int row = m0 + i * 16 + r16;
     rowok[i] = row < M;
-    ap[i] = A + (long)(rowok[i] ? row : 0) * lda + kq;
+    ap[i] = A + (long)(KF ? min(row, M - 1) : (rowok[i] ? row : 0)) * lda + kq;
   }
   f32x4 acc[MI];
 #pragma unroll
@@ -1819,18 +1835,28 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_bf16_kernel(int M, int N,
     bf16x8 a[UNR][MI], b[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int k = (s0 + u * NW) * 32;
-      const bool kok = k + kq < K;  // K % 8 == 0: a lane's 8-chunk is all in or all out
-      b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+      if constexpr (KF) {
+        const int k = min(s0 + u * NW, nsteps - 1) * 32;
+        b[u] = *reinterpret_cast<const bf16x8*>(bp + k);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
-        a[u][i] = (rowok[i] && kok) ? *reinterpret_cast<const bf16x8*>(ap[i] + k) : bf16x8{};
+        for (int i = 0; i < MI; ++i) a[u][i] = *reinterpret_cast<const bf16x8*>(ap[i] + k);
+      } else {
+        const int k = (s0 + u * NW) * 32;
+        const bool kok = k + kq < K;  // K % 8 == 0: a lane's 8-chunk is all in or all out
+        b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          a[u][i] = (rowok[i] && kok) ? *reinterpret_cast<const bf16x8*>(ap[i] + k) : bf16x8{};
+      }
     }
+    if (KF && s0 == wave) epi_prefetch_clamped(e, M, N, erow, ecol, ep);
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
+      if (!KF || s0 + u * NW < nsteps)  // wave-uniform
 #pragma unroll
-      for (int i = 0; i < MI; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
+        for (int i = 0; i < MI; ++i) acc[i] = mfma16(a[u][i], b[u], acc[i]);
   }
+  if (KF && wave >= nsteps) epi_prefetch_clamped(e, M, N, erow, ecol, ep);  // waves with no K step
   // D[row 4g+r][col c16] of each 16x16 tile
   const int g = lane >> 4;
 #pragma unroll
@@ -2130,6 +2156,16 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   return (int)s;
 }
 
+// SMER_SKINNY_KF=0: the skinny bf16 kernel's guarded-load form at every K (A/B runs)
+static bool smer_skinny_kf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_SKINNY_KF");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <bool AK, bool BKC>
 static void launch_bf16(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                         const GemmEpi& e, void* ws, size_t ws_bytes, hipStream_t s,
@@ -2140,23 +2176,26 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     // 16-row workgroups while that keeps the grid within two per CU
     // (per-workgroup load time, not the grid, bounds a decode Linear)
     const bool m16 = smer_skinny16_enabled() && (long)ntn * ((M + 15) / 16) <= smer_skinny16_cap() * smer_num_cus();
+    const bool kf = K % 32 == 0 && smer_skinny_kf();
+#define SKB(U, MI)                                                                                     \
+  do {                                                                                                 \
+    if (kf)                                                                                            \
+      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, U, MI, true>), grid, dim3(512), 0, s, M, N, K,    \
+                         (const bf16*)A, lda, (const bf16*)B, ldb, e);                                 \
+    else                                                                                               \
+      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, U, MI, false>), grid, dim3(512), 0, s, M, N, K,   \
+                         (const bf16*)A, lda, (const bf16*)B, ldb, e);                                 \
+  } while (0)
     if (m16) {
       const dim3 grid(ntn, (M + 15) / 16);
-      if (nsteps > 16)
-        hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 4, 1>), grid, dim3(512), 0, s, M, N, K,
-                           (const bf16*)A, lda, (const bf16*)B, ldb, e);
-      else
-        hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 2, 1>), grid, dim3(512), 0, s, M, N, K,
-                           (const bf16*)A, lda, (const bf16*)B, ldb, e);
+      if (nsteps > 16) SKB(4, 1);
+      else SKB(2, 1);
       return;
     }
     const dim3 grid(ntn, (M + SK_BM - 1) / SK_BM);
-    if (nsteps > 16)  // 8 waves x 4 steps (16 waves would spill at 128 VGPRs)
-      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 4>), grid, dim3(512), 0, s, M, N, K,
-                         (const bf16*)A, lda, (const bf16*)B, ldb, e);
-    else
-      hipLaunchKernelGGL((gemm_skinny_bf16_kernel<8, 2>), grid, dim3(512), 0, s, M, N, K,
-                         (const bf16*)A, lda, (const bf16*)B, ldb, e);
+    if (nsteps > 16) SKB(4, 4);  // 8 waves x 4 steps (16 waves would spill at 128 VGPRs)
+    else SKB(2, 4);
+#undef SKB
     return;
   }
   // large-M forward / dgrad: 256x256 tiles when they fill the chip
@@ -2585,7 +2624,14 @@ extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* 
 // sublayer adds) — then runs the K loop from LDS.  Saves the LayerNorm
 // launch and its HBM round trip per norm (3 of the ~11 launches per layer).
 // ---------------------------------------------------------------------------
-template <int NW, int UNR>
+// KF (K % 32 == 0, the decode shapes): the weight fragments, this wave's
+// rows and gamma / beta are loaded unconditionally (column / row / chunk
+// indices clamped: clamped rows are normalised too and dropped by the
+// epilogue's bounds; nothing is stored for them), and the epilogue's bias /
+// residual requested last -- the guarded loads (selects behind them) and the
+// epilogue prefetch first made every workgroup wait for a load before
+// issuing the next.  NC: 16-B row chunks per lane (K <= 512 NC).
+template <int NW, int UNR, int NC = LNR_MAXC, bool KF = false>
 __global__ __launch_bounds__(64 * NW) void gemm_skinny_ln_kernel(int M, int N, int K,
                                                                  const bf16* __restrict__ Y, long ldy,
                                                                  const float* __restrict__ gamma,
@@ -2603,22 +2649,69 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_ln_kernel(int M, int N, i
   const bool eth = tid < BM * 2;
   const bool pre = eth && epi_pre_ok(e, M, N, erow, ecol);
   EpiPre ep;
-  if (pre) epi_prefetch(e, erow, ecol, ep);
+  if (!KF && pre) epi_prefetch(e, erow, ecol, ep);
   // the weight fragments of the first K round are requested before the
   // LayerNorm prologue, so their HBM latency overlaps it (else two
   // dependent round trips: rows, then weights)
   const int r16 = lane & 15, kq = (lane >> 4) * 8;
   const int ncol = n0 + r16;
   const bool colok = ncol < N;
-  const bf16* bp = B + (long)(colok ? ncol : 0) * ldb + kq;
+  const bf16* bp = B + (long)(KF ? min(ncol, N - 1) : (colok ? ncol : 0)) * ldb + kq;
   const int nsteps = (K + 31) / 32;
   bf16x8 b0[UNR];
 #pragma unroll
   for (int u = 0; u < UNR; ++u) {
     const int k = (wave + u * NW) * 32;
-    b0[u] = (colok && k + kq < K) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
+    if constexpr (KF) b0[u] = *reinterpret_cast<const bf16x8*>(bp + min(k, (nsteps - 1) * 32));
+    else b0[u] = (colok && k + kq < K) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
   }
   const int nch = K >> 3;
+  if constexpr (KF) {
+    constexpr int RPW = BM / NW;  // rows per wave
+    bf16x8 yv[RPW][NC];
+    float4 gv[NC][2], bv[NC][2];
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const bf16* yr = Y + (long)min(m0 + wave + NW * j, M - 1) * ldy;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) yv[j][c] = *reinterpret_cast<const bf16x8*>(yr + 8 * min(lane + 64 * c, nch - 1));
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = min(lane + 64 * c, nch - 1);
+      gv[c][0] = *reinterpret_cast<const float4*>(gamma + ch * 8);
+      gv[c][1] = *reinterpret_cast<const float4*>(gamma + ch * 8 + 4);
+      bv[c][0] = *reinterpret_cast<const float4*>(beta + ch * 8);
+      bv[c][1] = *reinterpret_cast<const float4*>(beta + ch * 8 + 4);
+    }
+    epi_prefetch_clamped(e, M, N, erow, ecol, ep);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+      const int rr = wave + NW * j, row = m0 + rr;
+      char* dst = xs + rr * xs_ld;
+      float v[NC][8], mu, rs;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = (float)yv[j][c][i];
+      ln_stats_loaded<NC>(v, K, eps, lane, mu, rs);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ch = lane + 64 * c;
+        if (ch < nch) {
+          const float g[8] = {gv[c][0].x, gv[c][0].y, gv[c][0].z, gv[c][0].w,
+                              gv[c][1].x, gv[c][1].y, gv[c][1].z, gv[c][1].w};
+          const float b[8] = {bv[c][0].x, bv[c][0].y, bv[c][0].z, bv[c][0].w,
+                              bv[c][1].x, bv[c][1].y, bv[c][1].z, bv[c][1].w};
+          bf16x8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = (bf16)ln_apply(v[c][i], mu, rs, g[i], b[i]);
+          *reinterpret_cast<bf16x8*>(dst + ch * 16) = o;
+          if (X && blockIdx.x == 0 && row < M) *reinterpret_cast<bf16x8*>(X + (long)row * ldx + ch * 8) = o;
+        }
+      }
+    }
+  } else {
   for (int rr = wave; rr < BM; rr += NW) {  // wave-uniform
     const int row = m0 + rr;
     char* dst = xs + rr * xs_ld;
@@ -2646,6 +2739,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_ln_kernel(int M, int N, i
       for (int ch = lane; ch < nch; ch += 64) *reinterpret_cast<bf16x8*>(dst + ch * 16) = bf16x8{};
     }
   }
+  }
   __syncthreads();
   const char* ap = xs + r16 * xs_ld + kq * 2;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2656,11 +2750,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_skinny_ln_kernel(int M, int N, i
       const int k = (s0 + u * NW) * 32;
       const bool kok = k + kq < K;
       if (s0 == wave) b[u] = b0[u];
+      else if (KF) b[u] = *reinterpret_cast<const bf16x8*>(bp + min(k, (nsteps - 1) * 32));
       else b[u] = (colok && kok) ? *reinterpret_cast<const bf16x8*>(bp + k) : bf16x8{};
-      a[u] = kok ? *reinterpret_cast<const bf16x8*>(ap + 2 * k) : bf16x8{};
+      if (KF) a[u] = *reinterpret_cast<const bf16x8*>(ap + 2 * min(k, (nsteps - 1) * 32));
+      else a[u] = kok ? *reinterpret_cast<const bf16x8*>(ap + 2 * k) : bf16x8{};
     }
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) acc = mfma16(a[u], b[u], acc);
+    for (int u = 0; u < UNR; ++u)
+      if (!KF || s0 + u * NW < nsteps)  // wave-uniform
+        acc = mfma16(a[u], b[u], acc);
   }
   const int g = lane >> 4;
 #pragma unroll
@@ -2708,12 +2806,19 @@ extern "C" int smer_linear_decode_ln(int M, int N, int K, const void* Y, long ld
   const dim3 grid((N + SK_BN - 1) / SK_BN, (M + 15) / 16);
   const size_t lds = 16 * (2 * (size_t)K + 32);
   hipStream_t s = (hipStream_t)stream;
-  if ((K + 31) / 32 > 16)
-    hipLaunchKernelGGL((gemm_skinny_ln_kernel<8, 4>), grid, dim3(512), lds, s, M, N, K, (const bf16*)Y, ldy,
-                       gamma, beta, eps, (bf16*)X, ldx, (const bf16*)W, ldw, e);
-  else
-    hipLaunchKernelGGL((gemm_skinny_ln_kernel<8, 2>), grid, dim3(512), lds, s, M, N, K, (const bf16*)Y, ldy,
-                       gamma, beta, eps, (bf16*)X, ldx, (const bf16*)W, ldw, e);
+#define SKLN(U, NC, KF)                                                                                  \
+  hipLaunchKernelGGL((gemm_skinny_ln_kernel<8, U, NC, KF>), grid, dim3(512), lds, s, M, N, K, (const bf16*)Y, \
+                     ldy, gamma, beta, eps, (bf16*)X, ldx, (const bf16*)W, ldw, e)
+  if (K % 32 == 0 && smer_skinny_kf()) {
+    if (K <= 512) SKLN(2, 1, true);
+    else if (K <= 1024) SKLN(4, 2, true);
+    else SKLN(4, 4, true);
+  } else if ((K + 31) / 32 > 16) {
+    SKLN(4, LNR_MAXC, false);
+  } else {
+    SKLN(2, LNR_MAXC, false);
+  }
+#undef SKLN
   SMER_CHECK_LAUNCH("smer_linear_decode_ln");
   return SMER_OK;
 }
@@ -2773,10 +2878,12 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, 
   const int col = n0 + cq;
   const int mrows = min(SKF_BM, M - m0);
   const float* bp = B + (long)min(col, N - 1) * ldb;
-  // loads in the order they are needed (vmcnt counts in order): this wave's
-  // first row (and the LayerNorm's gamma / beta), then the weights, so the
-  // row work waits for the row alone.  Chunk indices are clamped, not
-  // guarded: a clamped chunk rereads (and rewrites) the row's last one.
+  // this wave's first row (and the LayerNorm's gamma / beta) requested up
+  // front with the weights (hipcc issues the weight loads first whatever the
+  // source order -- a memory clobber or sched_barrier between them does not
+  // keep the rows ahead -- so the row work still waits for both: vmcnt
+  // counts in order).  Chunk indices are clamped, not guarded: a clamped
+  // chunk rereads (and rewrites) the row's last one.
   const int nch = K >> 3, n4 = K >> 2;
   const float* y0 = Y + (long)(m0 + min(wave, mrows - 1)) * ldy;
   float4 t[SKF_UNR];  // !LN: the first row, 16 B per lane per chunk
@@ -2793,9 +2900,6 @@ __global__ __launch_bounds__(64 * SKF_NW) void gemm_skinny_ln_f32_kernel(int M, 
 #pragma unroll
     for (int c = 0; c < SKF_UNR; ++c) t[c] = *reinterpret_cast<const float4*>(y0 + 4 * min(lane + 64 * c, n4 - 1));
   }
-  // compiler memory barrier: hipcc otherwise sinks the row loads behind the
-  // weight loads (into the row loop), and the row work then waits for both
-  asm volatile("" ::: "memory");
   float4 b[SKF_UNR];
 #pragma unroll
   for (int u = 0; u < SKF_UNR; ++u) {
