@@ -530,12 +530,18 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
   const float c = scale * LOG2E_F;
 
   bf16x8 kf[KG][C::NS], vf[KG][C::NS];
-  bool kvalid[KG];
+  // padded keys get no gradient: their dK / dV rows are written as zeros.
+  // The padding bytes are kept raw until the epilogue (a test right behind
+  // the load made every workgroup wait for it before its K / V loads)
+  // (loaded unconditionally -- from K's own bytes without a mask, ignored
+  // through kmask -- as a load under a branch left a phi copy that waited)
+  uint32_t kpad[KG];
+  const uint8_t* kpb = kpm ? kpm + (long)b * Lk : reinterpret_cast<const uint8_t*>(k);
+  const uint32_t kmask = kpm ? 0xFFu : 0u;
 #pragma unroll
   for (int gk = 0; gk < KG; ++gk) {
     const int kj = k0w + gk * 16 + c16;
-    // padded keys get no gradient: their dK / dV rows are written as zeros
-    kvalid[gk] = kj < Lk && !(kpm && kpm[(long)b * Lk + min(kj, Lk - 1)]);
+    kpad[gk] = kpb[min(kj, Lk - 1)];
     long row = (long)(b * Lk + min(kj, Lk - 1));
 #pragma unroll
     for (int s = 0; s < C::NS; ++s) {
@@ -705,14 +711,15 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
     if (kj >= Lk) continue;
     bf16* dkr = dk + (long)(b * Lk + kj) * lddk + h * D;
     bf16* dvr = dv + (long)(b * Lk + kj) * lddv + h * D;
+    const bool kvalid = (kpad[gk] & kmask) == 0u;
     // select, not multiply: a padded key's unmasked P may have overflowed
 #pragma unroll
     for (int dt = 0; dt < C::NDT; ++dt) {
       bf16x4 wk, wv;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        wk[r] = (bf16)(kvalid[gk] ? adk[gk][dt][r] * scale : 0.f);
-        wv[r] = (bf16)(kvalid[gk] ? adv[gk][dt][r] * (DROP ? drop_scale : 1.f) : 0.f);
+        wk[r] = (bf16)(kvalid ? adk[gk][dt][r] * scale : 0.f);
+        wv[r] = (bf16)(kvalid ? adv[gk][dt][r] * (DROP ? drop_scale : 1.f) : 0.f);
       }
       *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
       *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;

@@ -119,18 +119,15 @@ __global__ __launch_bounds__(256) void ln_fwd_rows_kernel(int M, int N, const bf
   for (int r = 0; r < RPW; ++r) {
     const long row = min(row0 + r, M - 1);
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
-      if (lane + 64 * c < nch)
-        raw[r][c] = *reinterpret_cast<const bf16x8*>(x + row * ldx + (lane + 64 * c) * 8);
+    for (int c = 0; c < NC; ++c)  // chunk clamped, not guarded (a guarded load waited behind it)
+      raw[r][c] = *reinterpret_cast<const bf16x8*>(x + row * ldx + min(lane + 64 * c, nch - 1) * 8);
   }
   float gb[NC][16];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    const int ch = lane + 64 * c;
-    if (ch < nch) {
-      Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
-      Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
-    }
+    const int ch = min(lane + 64 * c, nch - 1);
+    Vec8<float>::load(gamma + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][0]));
+    Vec8<float>::load(beta + ch * 8, *reinterpret_cast<float(*)[8]>(&gb[c][8]));
   }
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
@@ -236,12 +233,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
   // statistics) before this batch's math, so a wave keeps two batches in
   // flight; every conversion / validity select happens at unpack time (a
   // select right behind a load makes hipcc wait for it there)
-  constexpr bool PF = PFB && sizeof(T) == 2;  // PFB: several batches per wave (64-row blocks)
+  // (bf16 without PFB -- one batch per wave -- fetches its batch raw the
+  // same way, just not a batch ahead: the guarded, converted loads of the
+  // plain path made hipcc wait behind each load)
+  constexpr bool RAW = sizeof(T) == 2;
+  constexpr bool PF = PFB && RAW;  // PFB: several batches per wave (64-row blocks)
   constexpr int DW = DYF ? 2 : 1;  // 16-B words of dy per 8 columns
-  uint4 px[PF ? RB : 1][NC], pd[PF ? RB : 1][NC][DW];
-  float pmu[PF ? RB : 1], prs[PF ? RB : 1];
+  uint4 px[RAW ? RB : 1][NC], pd[RAW ? RB : 1][NC][DW];
+  float pmu[RAW ? RB : 1], prs[RAW ? RB : 1];
   auto fetch = [&](int rb) {
-    if constexpr (PF) {
+    if constexpr (RAW) {
 #pragma unroll
       for (int u = 0; u < RB; ++u) {
         const int row = min(r0 + wave + 4 * (rb + u), M - 1);
@@ -268,7 +269,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
   for (int rb = 0; rb < rows_per_blk / 4; rb += RB) {
     float xh[RB][NC][8], gd[RB][NC][8], mu[RB], rs[RB];
     bool ok[RB];
-    if constexpr (PF) {
+    if constexpr (RAW && !PF) fetch(rb);
+    if constexpr (RAW) {
 #pragma unroll
       for (int u = 0; u < RB; ++u) {
         const int row = r0 + wave + 4 * (rb + u);
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
           }
         }
       }
-      if (rb + RB < rows_per_blk / 4) fetch(rb + RB);
+      if (PF && rb + RB < rows_per_blk / 4) fetch(rb + RB);
     } else {
 #pragma unroll
       for (int u = 0; u < RB; ++u) {
