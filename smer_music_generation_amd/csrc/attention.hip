@@ -1457,22 +1457,45 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
   // at all for a row with <= 1 key: softmax over one key is 1 whatever q,
   // e.g. a decode session's dummy rows)
   const bf16* wr = dq.wq + (long)(h * D + d) * dq.ldw + part * KT;
-  bf16x8 wv[KT / 8];
-  if (need_q) {
+  // every load of the prologue issued before any of it is used, all
+  // unconditional (chunk indices clamped; every wave reads the row and
+  // gamma / beta, wave 0 normalises): the guarded loads and the gamma / beta
+  // reads inside the normalisation made each block wait for one load after
+  // another.  Same arithmetic as ln_row_stats / ln_apply.
+  constexpr int NC = (DM + 511) / 512;  // 16-B chunks per lane
+  constexpr int NCH = DM / 8;
+  bf16x8 yv[NC];
+  float4 gv[NC][2], bv[NC][2];
 #pragma unroll
-    for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+  for (int c = 0; c < NC; ++c) {
+    const int ch = min(lane + 64 * c, NCH - 1);
+    yv[c] = *reinterpret_cast<const bf16x8*>(dq.y + (long)r * dq.ldy + ch * 8);
+    gv[c][0] = *reinterpret_cast<const float4*>(dq.gamma + ch * 8);
+    gv[c][1] = *reinterpret_cast<const float4*>(dq.gamma + ch * 8 + 4);
+    bv[c][0] = *reinterpret_cast<const float4*>(dq.beta + ch * 8);
+    bv[c][1] = *reinterpret_cast<const float4*>(dq.beta + ch * 8 + 4);
   }
-  if (wave == 0) {
-    float v[LNR_MAXC][8], mu, rs;
-    ln_row_stats<bf16>(dq.y + (long)r * dq.ldy, dq.dmodel, dq.eps, lane, v, mu, rs);
+  bf16x8 wv[KT / 8];
 #pragma unroll
-    for (int c = 0; c < LNR_MAXC; ++c) {
+  for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+  if (wave == 0) {
+    float v[NC][8], mu, rs;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = (float)yv[c][i];
+    ln_stats_loaded<NC>(v, DM, dq.eps, lane, mu, rs);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
       const int ch = lane + 64 * c;
-      if (ch < (dq.dmodel >> 3)) {
+      if (ch < NCH) {
+        const float g[8] = {gv[c][0].x, gv[c][0].y, gv[c][0].z, gv[c][0].w,
+                            gv[c][1].x, gv[c][1].y, gv[c][1].z, gv[c][1].w};
+        const float b[8] = {bv[c][0].x, bv[c][0].y, bv[c][0].z, bv[c][0].w,
+                            bv[c][1].x, bv[c][1].y, bv[c][1].z, bv[c][1].w};
         bf16x8 o;
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          o[i] = (bf16)ln_apply(v[c][i], mu, rs, dq.gamma[ch * 8 + i], dq.beta[ch * 8 + i]);
+        for (int i = 0; i < 8; ++i) o[i] = (bf16)ln_apply(v[c][i], mu, rs, g[i], b[i]);
         *reinterpret_cast<bf16x8*>(xs + ch * 8) = o;
         if (h == 0 && dq.x_out) *reinterpret_cast<bf16x8*>(dq.x_out + (long)r * dq.ldx + ch * 8) = o;
       }
@@ -1568,18 +1591,21 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   } else {
     load16b<T>(q + (long)r * ldq + h * (LPK * VEC) + sub * VEC, qv);
   }
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) qv[i] *= scale;
   // (QP: requesting the first key step's K / V before the query prologue
   // measured slower, 368 vs 336 us per decode step, and at C5's 4096-key
-  // memories 46.4k vs 47.5k tokens/s: issued after it)
-  if (PIPE && nk > kb) load_step(kb, kr, vr);
+  // memories 46.4k vs 47.5k tokens/s: issued after it.  Without the
+  // prologue the first step is requested before q is scaled, in both forms:
+  // scaling q first made every block wait for q before its K / V loads.)
+  if ((PIPE || QP == 0) && nk > kb) load_step(kb, kr, vr);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) qv[i] *= scale;
   for (int j0 = kb; j0 < nk; j0 += KPB * UNR) {
     uint4 kn[UNR], vn[UNR];
     if constexpr (PIPE) {
       if (j0 + KPB * UNR < nk) load_step(j0 + KPB * UNR, kn, vn);
     } else {
-      load_step(j0, kr, vr);
+      if (QP != 0 || j0 != kb) load_step(j0, kr, vr);
     }
     float sc[UNR];
     float mx = m;
