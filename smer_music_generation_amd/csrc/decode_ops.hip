@@ -348,19 +348,24 @@ __device__ double seq_sum(const double* a, int n) {
   for (; i < n; ++i) t += a[i];
   return t;
 }
-// c[i] = a[0] + ... + a[i], sequential (np.cumsum); returns c[n - 1]
+// c[i] = a[0] + ... + a[i], sequential (np.cumsum); returns c[n - 1].  A
+// batch's 8 sums are formed before its 8 stores (a store right behind each
+// add stalled on it: 25.7 vs 13.6 cycles per element for the plain sum)
 __device__ double seq_cumsum(const double* a, double* c, int n) {
   double t = 0.;
   int i = 0;
   for (; i + 8 <= n; i += 8) {
-    double x[8];
+    double x[8], r[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = a[i + j];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       t += x[j];
-      c[i + j] = t;
+      r[j] = t;
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[i + j] = r[j];
   }
   for (; i < n; ++i) {
     t += a[i];
@@ -383,6 +388,67 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
 template <int X>
 __device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
   return ((uint64_t)lane_xor<X>((uint32_t)(v >> 32)) << 32) | lane_xor<X>((uint32_t)v);
+}
+
+// bitonic sort, descending, of 64 E keys held E per lane (element s = lane
+// * E + e): partners at distance >= E sit in lane ^ (dist / E), nearer ones
+// in the same lane
+template <int E>
+__device__ __forceinline__ void sort_desc(uint64_t (&kv)[E], int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      if (jj >= E) {
+        const int lx = jj / E;
+        const bool lower = (lane & lx) == 0;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          const int e = lane * E + j;
+          const bool desc = (e & k) == 0;
+          uint64_t o;
+          switch (lx) {
+            case 1: o = lane_xor64<1>(kv[j]); break;
+            case 2: o = lane_xor64<2>(kv[j]); break;
+            case 4: o = lane_xor64<4>(kv[j]); break;
+            case 8: o = lane_xor64<8>(kv[j]); break;
+            case 16: o = lane_xor64<16>(kv[j]); break;
+            default: o = lane_xor64<32>(kv[j]); break;
+          }
+          const uint64_t mx = kv[j] > o ? kv[j] : o, mn = kv[j] > o ? o : kv[j];
+          kv[j] = (lower == desc) ? mx : mn;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          if (j & jj) continue;
+          const int e = lane * E + j;
+          const bool desc = (e & k) == 0;
+          const uint64_t a0 = kv[j], a1 = kv[j | jj];
+          const bool sw = desc ? a1 > a0 : a0 > a1;
+          kv[j] = sw ? a1 : a0;
+          kv[j | jj] = sw ? a0 : a1;
+        }
+      }
+    }
+  }
+}
+
+// fast path of the sampler: sort the first 64 E compacted keys (E per lane)
+// and gather the p of sort positions < NA into sp
+template <int E>
+__device__ __forceinline__ void fast_sort_gather(const uint64_t* kA, int lane, int NA, int (&sidx)[8], double* sp,
+                                                 const double* pe) {
+  uint64_t k[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) k[e] = kA[lane * E + e];
+  sort_desc<E>(k, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int s = lane * E + e;
+    sidx[e] = (int)(uint32_t)k[e];
+    if (s < NA) sp[s] = pe[sidx[e]];
+  }
 }
 
 // np.sum's pairwise order over a[0..n) with the leaves' eight accumulator
@@ -493,6 +559,7 @@ __global__ __launch_bounds__(64) void grammar_sample_kernel(
   __shared__ uint32_t key[624];
   __shared__ double pe[SMX];   // e, then p by vocabulary index
   __shared__ double sp[SMX];   // p in sort order, then the normalised cdf
+  __shared__ uint64_t kA[SMX];  // fast path: the compacted keys of set A
   __shared__ double bc[2];
   __shared__ int pwl[17];
   __shared__ __attribute__((aligned(16))) uint8_t tk[13 * SMX], tr[13 * SMX];  // keep / reject tables
@@ -530,18 +597,31 @@ __global__ __launch_bounds__(64) void grammar_sample_kernel(
     }
     for (int i = lane; i < V; i += 64) tcls[i] = cls[i];
   }
+  // a request's state row, mask targets and logits (indices clamped, not
+  // guarded: a guarded load waits right behind itself); request 0's with the
+  // batch above, request r + 1's under request r's work
+  auto fetch = [&](int r, int& sv, int& tgv, float (&lg)[8]) {
+    const int rr = min(r, R - 1);
+    sv = state[(long)rr * nst + min(lane, nst - 1)];
+    tgv = (int)targets[(long)rr * max_masks + min(lane, max_masks - 1)];
+    const float* lr = logits + (long)(2 * rr + 1) * ldl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lg[j] = lr[min(lane * 8 + j, V - 1)];
+  };
+  int sv_n, tgv_n;
+  float lg_n[8];
+  fetch(0, sv_n, tgv_n, lg_n);
   int pos = (int)mt[624];
   __syncthreads();
   SSTAMP(1);
   int live = 0;
   for (int r = 0; r < R; ++r) {
     int32_t* st = state + (long)r * nst;
-    const int sv = lane < nst ? st[lane] : 0;
-    const int tgv = lane < max_masks ? (int)targets[(long)r * max_masks + lane] : 0;
-    const float* lr = logits + (long)(2 * r + 1) * ldl;
+    const int sv = sv_n, tgv = tgv_n;
     float lg8[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) lg8[j] = lr[min(lane * 8 + j, V - 1)];
+    for (int j = 0; j < 8; ++j) lg8[j] = lg_n[j];
+    fetch(r + 1, sv_n, tgv_n, lg_n);
     if (__shfl(sv, ST_DONE, 64)) continue;  // wave-uniform
     const int flags = __shfl(sv, ST_FLAGS, 64), len = __shfl(sv, ST_LEN, 64),
               midx = __shfl(sv, ST_MIDX, 64), nmask = __shfl(sv, ST_NMASK, 64),
@@ -587,68 +667,106 @@ __global__ __launch_bounds__(64) void grammar_sample_kernel(
       const int i = lane * 8 + j;
       if (i < V) pe[i] = pe[i] / T;
     }
-    // bitonic sort of the 512 keys, descending, in registers: partners at
-    // distance >= 8 sit in lane ^ (dist / 8), nearer ones in the same lane
+    // The sort order, the sorted p and the cdf.  Fast path: the elements
+    // with x > -100 (set A: kept logits) sorted alone on a 64 / 128 / 256-key
+    // network; the rest all equal -100 (masked, or kept at exactly -100: set
+    // B, one shared p) and follow in descending index order, and when some
+    // kept logit is >= -60 their p is below 2^-54 of A's sum, so adding them
+    // leaves every cdf value past A at t_A: the cdf of A ends at t_A / t_A =
+    // 1.0 exactly, every draw u < 1 lands in A, and B is never needed.  Any
+    // kept logit below -100, none >= -60, no A, or a pB check that fails
+    // takes the full 512-key path (numpy's arithmetic either way).
+    double cd[8];
+    int sidx[8];
+    double total;
+    bool fast;
+    {
+      uint32_t am = 0u;
+      bool c_any = false, hi = false;
 #pragma unroll
-    for (int k = 2; k <= SMX; k <<= 1) {
+      for (int j = 0; j < 8; ++j) {
+        const int i = lane * 8 + j;
+        const float x = (i < V && kp[i]) ? lg8[j] : -100.f;
+        if (i < V && x > -100.f) am |= 1u << j;
+        if (i < V && x < -100.f) c_any = true;
+        if (i < V && x >= -60.f) hi = true;
+      }
+      fast = !__any(c_any) && __any(hi) && __any(am != 0u);
+      if (fast) {
+        // compact A's keys into LDS (prefix over lanes), pad to the network size
+        int incl = __popc(am);
 #pragma unroll
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        if (jj >= 8) {
-          const int lx = jj >> 3;
-          const bool lower = (lane & lx) == 0;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int t = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += t;
+        }
+        const int NA = __shfl(incl, 63, 64);
+        int pos = incl - __popc(am);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int e = lane * 8 + j;
-            const bool desc = (e & k) == 0;
-            uint64_t o;
-            switch (lx) {
-              case 1: o = lane_xor64<1>(kv[j]); break;
-              case 2: o = lane_xor64<2>(kv[j]); break;
-              case 4: o = lane_xor64<4>(kv[j]); break;
-              case 8: o = lane_xor64<8>(kv[j]); break;
-              case 16: o = lane_xor64<16>(kv[j]); break;
-              default: o = lane_xor64<32>(kv[j]); break;
-            }
-            const uint64_t mx = kv[j] > o ? kv[j] : o, mn = kv[j] > o ? o : kv[j];
-            kv[j] = (lower == desc) ? mx : mn;
-          }
+        for (int j = 0; j < 8; ++j)
+          if (am & (1u << j)) kA[pos++] = kv[j];
+        const int E = NA <= 64 ? 1 : NA <= 128 ? 2 : NA <= 256 ? 4 : 8;
+        for (int q = NA + lane; q < 64 * E; q += 64) kA[q] = 0ull;  // below every key
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { cd[j] = -1.0; sidx[j] = 0; }
+        if (E == 1) fast_sort_gather<1>(kA, lane, NA, sidx, sp, pe);
+        else if (E == 2) fast_sort_gather<2>(kA, lane, NA, sidx, sp, pe);
+        else if (E == 4) fast_sort_gather<4>(kA, lane, NA, sidx, sp, pe);
+        else fast_sort_gather<8>(kA, lane, NA, sidx, sp, pe);
+        // p of a B element (all equal), if any: the first one
+        uint32_t bmask = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (lane * 8 + j < V && !(am & (1u << j))) bmask |= 1u << j;
+        const uint64_t bm = __ballot(bmask != 0u);
+        double pB = 0.;
+        if (bm) {
+          const int bl = __builtin_ctzll(bm);
+          const int bj = __builtin_ctz((uint32_t)__shfl((int)bmask, bl, 64));
+          pB = pe[bl * 8 + bj];
+        }
+        __syncthreads();
+        if (lane == 0) bc[0] = seq_cumsum(sp, sp, NA);
+        __syncthreads();
+        SSTAMP(7);
+        total = bc[0];
+        if (pB * 18014398509481984.0 > total) {  // 2^54: the B terms would not vanish
+          fast = false;
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (j & jj) continue;
-            const int e = lane * 8 + j;
-            const bool desc = (e & k) == 0;
-            const uint64_t a0 = kv[j], a1 = kv[j | jj];
-            const bool sw = desc ? a1 > a0 : a0 > a1;
-            kv[j] = sw ? a1 : a0;
-            kv[j | jj] = sw ? a0 : a1;
+          for (int e = 0; e < 8; ++e) {
+            const int s = lane * E + e;
+            if (e < E && s < NA) cd[e] = sp[s] / total;
           }
         }
       }
     }
-    __syncthreads();
-    SSTAMP(5);
-    // p in sort order (slot s = lane * 8 + j holds sort position s)
-    int sidx[8];
+    if (!fast) {
+      // the full path: bitonic sort of all 512 keys in registers
+      sort_desc<8>(kv, lane);
+      __syncthreads();
+      SSTAMP(5);
+      // p in sort order (slot s = lane * 8 + j holds sort position s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int s = lane * 8 + j;
-      sidx[j] = (int)(uint32_t)kv[j];
-      sp[s] = s < V ? pe[sidx[j]] : 0.;
+      for (int j = 0; j < 8; ++j) {
+        const int s = lane * 8 + j;
+        sidx[j] = (int)(uint32_t)kv[j];
+        sp[s] = s < V ? pe[sidx[j]] : 0.;
+      }
+      __syncthreads();
+      SSTAMP(6);
+      if (lane == 0) bc[0] = seq_cumsum(sp, sp, V);
+      __syncthreads();
+      SSTAMP(7);
+      total = bc[0];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = lane * 8 + j;
+        cd[j] = s < V ? sp[s] / total : 2.0;
+      }
     }
-    __syncthreads();
-    SSTAMP(6);
-    if (lane == 0) bc[0] = seq_cumsum(sp, sp, V);
-    __syncthreads();
-    SSTAMP(7);
-    const double total = bc[0];
     const bool bad = !(fabs(total - 1.0) <= 1e-9);  // the host path hands such rows to np.random.choice
-    double cd[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int s = lane * 8 + j;
-      cd[j] = s < V ? sp[s] / total : 2.0;
-    }
     // draws (the reference's redraw loop: up to 11 redraws, the last kept):
     // the first sort position whose cdf exceeds u
     auto draw = [&]() -> int {

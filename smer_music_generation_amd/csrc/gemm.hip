@@ -231,7 +231,13 @@ __device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int la
 }
 }  // namespace
 
-template <bool AK, bool BKC, bool GL>
+// NSTG = 3 / 4 (weight gradients, LDS-DMA, one workgroup per CU): an
+// NSTG-stage LDS ring, each k-step's tiles requested NSTG - 1 steps ahead and
+// waited with a counted vmcnt before a raw barrier (the 2-stage form waits at the end of
+// every k-step for the tiles it requested at its start: one HBM round trip
+// per 64 of K against ~1 k cycles of MFMA work).  Fragment reads are asm,
+// so hipcc's wait insertion does not see them.
+template <bool AK, bool BKC, bool GL, int NSTG = 2>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
                                                            const bf16* __restrict__ A, long lda,
                                                            const bf16* __restrict__ B, long ldb,
@@ -294,9 +300,17 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
     f32x4 accr[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
     const int nk = (k_end - k_begin + GBK - 1) / GBK;
+    static_assert(NSTG == 2 || ((NSTG == 3 || NSTG == 4) && GL && !AK && !BKC),
+                  "3 / 4 stages: LDS-DMA weight gradients only");
     if constexpr (GL) {
       stage_glds<AK>(smem, A, lda, M, m0, k_begin, tid);
       stage_glds<BKC>(smem + TILE_BYTES, B, ldb, N, n0, k_begin, tid);
+#pragma unroll
+      for (int p = 1; p < NSTG - 1; ++p)
+        if (NSTG > 2 && p < nk) {
+          stage_glds<AK>(smem + p * 2 * TILE_BYTES, A, lda, M, m0, k_begin + p * GBK, tid);
+          stage_glds<BKC>(smem + p * 2 * TILE_BYTES + TILE_BYTES, B, ldb, N, n0, k_begin + p * GBK, tid);
+        }
     } else {
       if (!prefetched) {
         stage_load<AK>(ra, A, lda, M, k_end, m0, k_begin, tid);
@@ -305,12 +319,28 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
       stage_store<AK>(ra, smem, tid);
       stage_store<BKC>(rb, smem + TILE_BYTES, tid);
     }
-    __syncthreads();
+    if constexpr (NSTG > 2) {  // stage 0 landed (stages 1.. may stay in flight: 8 DMAs per thread each)
+      asm volatile("" ::: "memory");
+      const int ahead = min(NSTG - 2, nk - 1);
+      if (ahead >= 2) __builtin_amdgcn_s_waitcnt(0x4F70);       // vmcnt(16)
+      else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+      else __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
 
     for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
+      const int cur = NSTG == 2 ? kt & 1 : kt % NSTG;
       const bool more = kt + 1 < nk;
-      if constexpr (GL) {
+      if constexpr (NSTG > 2) {
+        if (kt + NSTG - 1 < nk) {
+          char* nb = smem + ((kt + NSTG - 1) % NSTG) * 2 * TILE_BYTES;
+          stage_glds<AK>(nb, A, lda, M, m0, k_begin + (kt + NSTG - 1) * GBK, tid);
+          stage_glds<BKC>(nb + TILE_BYTES, B, ldb, N, n0, k_begin + (kt + NSTG - 1) * GBK, tid);
+        }
+      } else if constexpr (GL) {
         if (more) {
           char* nb = smem + (cur ^ 1) * 2 * TILE_BYTES;
           stage_glds<AK>(nb, A, lda, M, m0, k_begin + (kt + 1) * GBK, tid);
@@ -375,7 +405,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         stage_store<AK>(ra, smem + (cur ^ 1) * 2 * TILE_BYTES, tid);
         stage_store<BKC>(rb, smem + (cur ^ 1) * 2 * TILE_BYTES + TILE_BYTES, tid);
       }
-      __syncthreads();
+      if constexpr (NSTG > 2) {
+        // this step's fragment reads done (the next step's DMA refills this
+        // stage), the next step's tiles landed: the stages requested after
+        // it (up to NSTG - 2 of them, 8 DMAs per thread each) may stay in flight
+        asm volatile("" ::: "memory");
+        const int ahead = min(NSTG - 2, nk - kt - 2);
+        if (ahead >= 2) __builtin_amdgcn_s_waitcnt(0x4070);       // vmcnt(16) lgkmcnt(0)
+        else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) lgkmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0x0070);                  // vmcnt(0) lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      } else {
+        __syncthreads();
+      }
     }
 
     // prefetch the next item's first K stage: its load latency hides behind
@@ -2120,6 +2163,19 @@ static long smer_skinny16_cap() {  // workgroups per CU (SMER_SKINNY16_CAP; A/B 
 // 1 = one per two CUs).  The weight gradients run on a second stream beside
 // the main chain: a smaller persistent grid leaves CUs (and LDS) to the main
 // stream's kernels and cuts the split-K slab bytes in proportion.
+// SMER_WGRAD_STAGES = 2 / 3 / 4: LDS stages of the 128x128 split-K weight
+// gradients at one resident workgroup per CU (A/B runs).  Default 2: the
+// deeper rings hold 96 / 128 KiB of LDS per CU, which the concurrent main-
+// stream kernels then cannot share (C2 step 13.28-13.33 ms at 2 stages,
+// 13.52-13.56 at 3, 13.61-13.62 at 4; two interleaved rounds, one box)
+static int smer_wgrad_stages() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD_STAGES");
+    v = e ? std::max(2, std::min(4, atoi(e))) : 2;
+  }
+  return v;
+}
 static long smer_wgrad_resident() {
   static int v = -1;
   if (v < 0) {
@@ -2310,10 +2366,36 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   const int grid = nwg > resident ? (int)(resident & ~7L) : (int)nwg;
   // LDS-DMA staging needs whole 64-deep K steps in every slice
   const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled();
-  auto kern = gl ? gemm_bf16_kernel<AK, BKC, true> : gemm_bf16_kernel<AK, BKC, false>;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 4 * TILE_BYTES,
-                     s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
-                     (float*)ws, split > 1 ? rs_part : rowsum);
+  if constexpr (!AK && !BKC) {
+    // weight gradients at one resident workgroup per CU: the 3-stage ring
+    const int ns = smer_wgrad_stages();
+    if (gl && split > 1 && smer_wgrad_resident() <= smer_num_cus() && ns > 2) {
+      static bool attr = false;
+      if (!attr) {
+        hipFuncSetAttribute((const void*)gemm_bf16_kernel<false, false, true, 3>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 6 * TILE_BYTES);
+        hipFuncSetAttribute((const void*)gemm_bf16_kernel<false, false, true, 4>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 8 * TILE_BYTES);
+        attr = true;
+      }
+      if (ns == 4)
+        hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, 4>), dim3(grid), dim3(256), 8 * TILE_BYTES, s,
+                           M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
+                           rs_part);
+      else
+        hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, 3>), dim3(grid), dim3(256), 6 * TILE_BYTES, s,
+                           M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
+                           rs_part);
+      goto reduce;
+    }
+  }
+  {
+    auto kern = gl ? gemm_bf16_kernel<AK, BKC, true> : gemm_bf16_kernel<AK, BKC, false>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 4 * TILE_BYTES,
+                       s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
+                       (float*)ws, split > 1 ? rs_part : rowsum);
+  }
+reduce:
   if (split > 1) {
     long n4 = ((long)M * N) / 4 + (rowsum ? M : 0);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,

@@ -524,9 +524,10 @@ def test_device_sampled_generation_all_matches_host_loop(golden_dir, precision):
 
 def test_device_sampler_draws_match_numpy_on_random_rows():
     """grammar_sample_kernel alone on random logit rows and states (many
-    rows, the MT19937 twist crossed several times): every drawn id equals the
-    host sampler's (sampling() + the redraw loop of _Span._draw) on the same
-    numpy stream, and the stream position afterwards is the same."""
+    rows, the MT19937 twist crossed several times, both of the kernel's sort
+    paths): every drawn id equals the host sampler's (sampling() + the redraw
+    loop of _Span._draw) on the same numpy stream, and the stream position
+    afterwards is the same."""
     from smer_music_generation_amd import ops as O
     from smer_music_generation_amd.generation import (grammar_spec, grammar_tables, reject_table,
                                                        sampling)
@@ -538,6 +539,15 @@ def test_device_sampler_draws_match_numpy_on_random_rows():
     rng = np.random.default_rng(3)
     n_rows = 400
     rows = (rng.standard_normal((n_rows, V)) * rng.uniform(0.5, 6.0, (n_rows, 1))).astype(np.float32)
+    # the kernel's two sort paths: kept logits all above -100 with some >= -60
+    # sort alone (fast path); rows with some kept logits below -100 or none
+    # >= -60 (around -80) take the full 512-key sort; some logits at exactly
+    # -100 tie kept elements with the masked ones.  (No row draws among the
+    # masked ones: their order is descending index on the device, numpy's
+    # unstable argsort order on the host -- DESIGN.md section 8.)
+    rows[7::10, ::13] = -130.0
+    rows[3::10] = rows[3::10] * 0.25 - 80.0
+    rows[5::10, ::17] = -100.0
     # states the kernel derives: flags / length / target chosen per row
     flag_sets = [(1, 5, 0), (2, 5, 0), (4, 5, 0), (8, 5, 0), (0, 1, 0), (0, 1, 1), (0, 5, 0), (0, 1, 4)]
     np.random.seed(11)
