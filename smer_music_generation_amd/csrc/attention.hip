@@ -283,12 +283,18 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       : nullptr;
   if (n_tiles > 0) {
     if constexpr (DROP && MIN) mw_next = mwp[0];
+    // the first tile's padding byte requested with its K / V (from K's own
+    // bytes without a mask, ignored through pmask): tested only after the
+    // tile has landed -- testing it at once cost every workgroup a round trip
+    const uint8_t* kpb = kp ? kp : reinterpret_cast<const uint8_t*>(kb);
+    const uint32_t pmask = kp ? 0xFFu : 0u;
+    const uint32_t pad0 = kpb[min(lane, Lk - 1)];
     tile_load<D>(rk, kb, ldk, 0, Lk, tid);
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
     if (tid < KVB) {  // wave 0
-      const float kbz = key_bias(tid);
+      const float kbz = (tid >= Lk || (pad0 & pmask)) ? -INFINITY : 0.f;
       kbias[0][tid] = kbz;
       const uint64_t any = __ballot(kbz != 0.f);
       if (tid == 0) kpad[0] = any != 0ull;
@@ -812,17 +818,22 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     for (int i = 0; i < C::NDT; ++i) adq[gq][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 rk[C::CPT], rv[C::CPT];
   if (n_tiles > 0) {
+    // first tile's padding byte requested with its K / V, tested after they
+    // land (see attn_fwd_bf16)
+    const uint8_t* kpb = kp ? kp : reinterpret_cast<const uint8_t*>(kb);
+    const uint32_t pmask = kp ? 0xFFu : 0u;
+    const uint32_t pad0 = kpb[min(lane, Lk - 1)];
+    if constexpr (use_mask) mw_next = mwp[0];
     tile_load<D>(rk, kb, ldk, 0, Lk, tid);
     tile_load<D>(rv, vb, ldv, 0, Lk, tid);
     tile_store<D>(rk, sm[0][0], tid);
     tile_store<D>(rv, sm[0][1], tid);
     if (tid < KVB) {  // wave 0
-      const float kbz = key_bias(tid);
+      const float kbz = (tid >= Lk || (pad0 & pmask)) ? -INFINITY : 0.f;
       kbias[0][tid] = kbz;
       const uint64_t any = __ballot(kbz != 0.f);
       if (tid == 0) kpad[0] = any != 0ull;
     }
-    if constexpr (use_mask) mw_next = mwp[0];
   }
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
