@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--n", type=int, default=50)
     ap.add_argument("--graph", action="store_true")
     ap.add_argument("--T", type=int, default=600, help="decoder cache capacity (max_tgt)")
+    ap.add_argument("--precision", default=None, help="fp32 / bf16 (default: the model's)")
     a = ap.parse_args()
     from smer_music_generation_amd import _lib
     from smer_music_generation_amd.decode import DecodeSession
@@ -25,7 +26,7 @@ def main():
     dev = torch.device("cuda", 0)
     m = bench.make_model(args, dev).eval()
     with torch.no_grad():
-        s = DecodeSession(m, a.R, a.S, a.T, use_graph=a.graph)
+        s = DecodeSession(m, a.R, a.S, a.T, precision=a.precision, use_graph=a.graph)
         s.prefill(list(range(a.R)), [[4] * a.S for _ in range(a.R)])
         s.step([(i, [5], 0) for i in range(a.R)])
         torch.cuda.synchronize()
