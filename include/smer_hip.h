@@ -250,6 +250,16 @@ int smer_attn_decode_split_f32(int n_rows, int H, int D, const void* q, long ldq
                                const void* vcache, long row_stride, long req_stride, long head_stride,
                                const int32_t* row_req, const int32_t* row_nkeys, float* part, float scale,
                                smer_stream_t stream);
+/* smer_attn_decode_split_f32 whose query is LN(y) . wq^T + bq (fp32,
+ * bits of smer_linear_decode_ln_f32's normalisation), both computed in the
+ * attention blocks: replaces smer_linear_decode_ln_f32 (cross-Q) + split
+ * attention for the fp32 plugin step at batch 1 (transformer.py:462 -> 459
+ * -> 463).  x_out <- LN(y) when given.  D == 64, dmodel == 512. */
+int smer_attn_decode_split_qln_f32(int n_rows, int H, int D, const float* y, long ldy, const float* gamma,
+                                   const float* beta, float eps, const float* wq, long ldw, const float* bq,
+                                   float* x_out, long ldx, int dmodel, const void* kcache, const void* vcache,
+                                   long row_stride, long req_stride, long head_stride, const int32_t* row_req,
+                                   const int32_t* row_nkeys, float* part, float scale, smer_stream_t stream);
 int smer_linear_decode_merge_f32(int M, int N, int K, const float* part, const void* W, long ldw,
                                  const float* bias, int relu, const void* residual, long ldr, void* C,
                                  long ldc, float* Cf, long ldcf, smer_stream_t stream);

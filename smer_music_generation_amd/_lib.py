@@ -65,6 +65,8 @@ SIGNATURES = {
                                           c_long, P, P, c_int, P]),
     "smer_attn_decode_split_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_long, c_long, c_long, P, P, P,
                                            c_float, P]),
+    "smer_attn_decode_split_qln_f32": (c_int, [c_int, c_int, c_int, P, c_long, P, P, c_float, P, c_long, P, P,
+                                               c_long, c_int, P, P, c_long, c_long, c_long, P, P, P, c_float, P]),
     "smer_linear_decode_merge_f32": (c_int, [c_int, c_int, c_int, P, P, c_long, P, c_int, P, c_long, P, c_long, P,
                                              c_long, P]),
     "smer_fp8_quantize_workspace": (c_size, []),

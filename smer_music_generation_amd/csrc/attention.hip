@@ -1443,23 +1443,25 @@ __device__ __forceinline__ float group_sum(float v) {
 // store it, the next sublayer's residual) and forms its head's D query
 // values as a bf16-rounded x . Wq_h^T + bq_h (fp32 dot products, 512 / D
 // threads per output), replacing the cross-Q Linear launch.
+// The fp32 form (dec_q_prologue_f32, the plugin's fp32 step at batch 1) keeps
+// every value in fp32, as the Linear it replaces.
 struct DecQ {
-  const bf16* y;
+  const void* y;  // the kernel's T (bf16 / fp32), as wq and x_out
   long ldy;
   const float* gamma;
   const float* beta;
   float eps;
-  const bf16* wq;  // [H*D rows, dmodel] (this head: rows h*D ..)
+  const void* wq;  // [H*D rows, dmodel] (this head: rows h*D ..)
   long ldw;
   const float* bq;
-  bf16* x_out;
+  void* x_out;
   long ldx;
   int dmodel;
 };
 
 template <int D, int NT, int DM>
 __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int tid, float* qs,
-                                               bf16* xs, bool need_q) {
+                                               bf16* xs, bool need_q, bool store_x) {
   constexpr int TPO = NT / D;    // threads per query value
   constexpr int KT = DM / TPO;   // K per thread (multiple of 8)
   const int lane = tid & 63, wave = tid >> 6;
@@ -1467,7 +1469,7 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
   // the head's weight row slice, requested before the row statistics (not
   // at all for a row with <= 1 key: softmax over one key is 1 whatever q,
   // e.g. a decode session's dummy rows)
-  const bf16* wr = dq.wq + (long)(h * D + d) * dq.ldw + part * KT;
+  const bf16* wr = static_cast<const bf16*>(dq.wq) + (long)(h * D + d) * dq.ldw + part * KT;
   // every load of the prologue issued before any of it is used, all
   // unconditional (chunk indices clamped; every wave reads the row and
   // gamma / beta, wave 0 normalises): the guarded loads and the gamma / beta
@@ -1480,7 +1482,7 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int ch = min(lane + 64 * c, NCH - 1);
-    yv[c] = *reinterpret_cast<const bf16x8*>(dq.y + (long)r * dq.ldy + ch * 8);
+    yv[c] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(dq.y) + (long)r * dq.ldy + ch * 8);
     gv[c][0] = *reinterpret_cast<const float4*>(dq.gamma + ch * 8);
     gv[c][1] = *reinterpret_cast<const float4*>(dq.gamma + ch * 8 + 4);
     bv[c][0] = *reinterpret_cast<const float4*>(dq.beta + ch * 8);
@@ -1508,7 +1510,7 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = (bf16)ln_apply(v[c][i], mu, rs, g[i], b[i]);
         *reinterpret_cast<bf16x8*>(xs + ch * 8) = o;
-        if (h == 0 && dq.x_out) *reinterpret_cast<bf16x8*>(dq.x_out + (long)r * dq.ldx + ch * 8) = o;
+        if (store_x && dq.x_out) *reinterpret_cast<bf16x8*>(static_cast<bf16*>(dq.x_out) + (long)r * dq.ldx + ch * 8) = o;
       }
     }
   }
@@ -1524,6 +1526,75 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
 #pragma unroll
     for (int w = 1; w < TPO; w <<= 1) acc += __shfl_xor(acc, w, 64);
     if (part == 0) qs[d] = (float)(bf16)(acc + dq.bq[h * D + d]);
+  } else if (part == 0) {
+    qs[d] = 0.f;
+  }
+  __syncthreads();
+}
+
+// fp32 form: x = LN(y) in fp32 (ln_stats_loaded / ln_apply: the bits of
+// gemm_skinny_ln_f32_kernel, whose x_out this replaces), q_h = x . Wq_h^T + bq_h
+// in fp32 without rounding.  The NT / D threads of one output read its weight
+// row interleaved (thread p takes the 16-B chunks p, p + TPO, ..: a row's
+// threads read contiguous 64 B per load), all DM / TPO weights of a thread
+// requested before the row statistics.
+template <int D, int NT, int DM>
+__device__ __forceinline__ void dec_q_prologue_f32(const DecQ& dq, int h, int r, int tid, float* qs, float* xs,
+                                                   bool need_q, bool store_x) {
+  constexpr int TPO = NT / D;            // threads per query value
+  constexpr int NJ = DM / (4 * TPO);     // 16-B weight chunks per thread
+  static_assert(DM % (4 * TPO) == 0 && DM % 8 == 0, "dec_q_prologue_f32: d_model");
+  const int lane = tid & 63, wave = tid >> 6;
+  const int d = tid / TPO, part = tid % TPO;
+  const float* wr = static_cast<const float*>(dq.wq) + (long)(h * D + d) * dq.ldw + 4 * part;
+  const float* yr = static_cast<const float*>(dq.y) + (long)r * dq.ldy;
+  constexpr int NC = (DM + 511) / 512;  // 32-B chunks per lane
+  constexpr int NCH = DM / 8;
+  float v[NC][8], g[NC][8], b[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int ch = min(lane + 64 * c, NCH - 1);
+    load8<float>(yr + ch * 8, 8, v[c]);
+    load8<float>(dq.gamma + ch * 8, 8, g[c]);
+    load8<float>(dq.beta + ch * 8, 8, b[c]);
+  }
+  float4 wv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) wv[j] = *reinterpret_cast<const float4*>(wr + 4 * TPO * j);
+  if (wave == 0) {
+    float mu, rs;
+    ln_stats_loaded<NC>(v, DM, dq.eps, lane, mu, rs);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < NCH) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = ln_apply(v[c][i], mu, rs, g[c][i], b[c][i]);
+        *reinterpret_cast<float4*>(xs + ch * 8) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(xs + ch * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        if (store_x && dq.x_out) {
+          float* xo = static_cast<float*>(dq.x_out) + (long)r * dq.ldx + ch * 8;
+          *reinterpret_cast<float4*>(xo) = make_float4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<float4*>(xo + 4) = make_float4(o[4], o[5], o[6], o[7]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (need_q) {  // block-uniform
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const float4 xv = *reinterpret_cast<const float4*>(xs + 4 * (TPO * j + part));
+      acc = fmaf(xv.x, wv[j].x, acc);
+      acc = fmaf(xv.y, wv[j].y, acc);
+      acc = fmaf(xv.z, wv[j].z, acc);
+      acc = fmaf(xv.w, wv[j].w, acc);
+    }
+#pragma unroll
+    for (int w = 1; w < TPO; w <<= 1) acc += __shfl_xor(acc, w, 64);
+    if (part == 0) qs[d] = acc + dq.bq[h * D + d];
   } else if (part == 0) {
     qs[d] = 0.f;
   }
@@ -1593,10 +1664,16 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   // measured 5.2 -> 5.7 TB/s at 4096 keys, slower at 1000)
   uint4 kr[UNR], vr[UNR];
   if constexpr (QP > 0) {  // QP = d_model of the query prologue
-    static_assert(sizeof(T) == 2, "the query prologue is bf16");
     __shared__ float qs[LPK * VEC];
-    __shared__ __attribute__((aligned(16))) bf16 xs[QP];
-    dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, SMER_DEC_QSKIP ? nk > 1 : true);
+    const bool need_q = SMER_DEC_QSKIP ? nk_all > 1 : true;
+    const bool store_x = h == 0 && (NS == 0 || blockIdx.z == 0);  // one block per row stores LN(y)
+    if constexpr (sizeof(T) == 2) {
+      __shared__ __attribute__((aligned(16))) bf16 xs[QP];
+      dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, need_q, store_x);
+    } else {
+      __shared__ __attribute__((aligned(16))) float xs[QP];
+      dec_q_prologue_f32<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, need_q, store_x);
+    }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) qv[i] = qs[sub * VEC + i];
   } else {
@@ -2086,6 +2163,39 @@ extern "C" int smer_attn_decode_split_f32(int n_rows, int H, int D, const void* 
   return SMER_OK;
 }
 
+// smer_attn_decode_split_f32 with the cross-attention query projection and
+// the LayerNorm in front of it computed in each block (dec_q_prologue_f32):
+// the plugin's fp32 step at batch 1, where the LN + Linear launch it replaces
+// was one of ~40 latency-bound launches per token.  x_out = LN(y) (the
+// merge's residual), written by the z = 0 block of head 0.  d_model 512.
+extern "C" int smer_attn_decode_split_qln_f32(int n_rows, int H, int D, const float* y, long ldy,
+                                              const float* gamma, const float* beta, float eps,
+                                              const float* wq, long ldw, const float* bq, float* x_out,
+                                              long ldx, int dmodel, const void* kcache, const void* vcache,
+                                              long row_stride, long req_stride, long head_stride,
+                                              const int32_t* row_req, const int32_t* row_nkeys, float* part,
+                                              float scale, smer_stream_t stream) {
+  SMER_REQUIRE(D == 64 && H > 0, "smer_attn_decode_split_qln_f32: head dim 64");
+  SMER_REQUIRE(dmodel == 512, "smer_attn_decode_split_qln_f32: d_model 512 (else: Linear + split attention)");
+  SMER_REQUIRE(y && gamma && beta && wq && bq && kcache && vcache && row_req && row_nkeys && part,
+               "smer_attn_decode_split_qln_f32: null pointer");
+  auto al = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  SMER_REQUIRE(al(y) && al(gamma) && al(beta) && al(wq) && al(kcache) && al(vcache) && al(part) &&
+                   (!x_out || al(x_out)) && ldy % 4 == 0 && ldw % 4 == 0 && ldx % 4 == 0 && row_stride % 4 == 0 &&
+                   req_stride % 4 == 0 && (head_stride <= 0 || head_stride % 4 == 0),
+               "smer_attn_decode_split_qln_f32: 16-B alignment / strides");
+  if (n_rows == 0) return SMER_OK;
+  if (head_stride <= 0) head_stride = D;
+  DecQ dq{y, ldy, gamma, beta, eps, wq, ldw, bq, x_out, ldx, dmodel};
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid(H, n_rows, 8);
+  hipLaunchKernelGGL((attn_decode_vec_kernel<float, 16, 2, 4, true, 512, 8>), grid, dim3(256), 0, s,
+                     (const float*)nullptr, 0L, (const float*)kcache, (const float*)vcache, row_stride, req_stride,
+                     head_stride, row_req, row_nkeys, (float*)nullptr, 0L, scale, dq, 0, part);
+  SMER_CHECK_LAUNCH("smer_attn_decode_split_qln_f32");
+  return SMER_OK;
+}
+
 extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, long ldy,
                                     const float* gamma, const float* beta, float eps, const void* wq,
                                     long ldw, const float* bq, void* x_out, long ldx, int dmodel,
@@ -2105,7 +2215,7 @@ extern "C" int smer_attn_decode_qln(int n_rows, int H, int D, const void* y, lon
                "smer_attn_decode_qln: 16-B alignment / strides");
   if (n_rows == 0) return SMER_OK;
   if (head_stride <= 0) head_stride = D;
-  DecQ dq{(const bf16*)y, ldy, gamma, beta, eps, (const bf16*)wq, ldw, bq, (bf16*)x_out, ldx, dmodel};
+  DecQ dq{y, ldy, gamma, beta, eps, wq, ldw, bq, x_out, ldx, dmodel};
   const int odd = smer_dec_odd_first();
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(H, n_rows);

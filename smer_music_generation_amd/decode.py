@@ -309,6 +309,11 @@ class DecodeSession:
         # merged in the out-projection's prologue): the unsplit form runs
         # 2 * R * H blocks, 16 at batch 1
         self._split_f32 = D == 64 and d <= 2048 and os.environ.get("SMER_DECODE_SPLIT_F32", "1") == "1"
+        # few rows (batch 1-2): LN1 + the cross-attention query projection
+        # computed inside the split attention blocks (one launch fewer per
+        # layer; each block re-reads its head's 128 KB of Wq from L2, so not
+        # for many rows)
+        qln = self._split_f32 and d == 512 and M <= 4 and os.environ.get("SMER_DECODE_QLN_F32", "1") == "1"
         y_prev = n_prev = None
         for li, L in enumerate(W.dec):
             cache = self.self_kv[li]
@@ -326,15 +331,23 @@ class DecodeSession:
                             row_stride=2 * d, req_stride=sstride, scale=scale)
             y1 = ops.linear(o, L.sa_ow, L.sa_ob, residual=x)
             x1 = torch.empty(M, d, dtype=dt, device=dev)
-            qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
             cc = self.cross_kv[li]
-            if self._split_f32:  # 8 key slices per (row, head), merged by the out-projection
+            if qln:
+                part = torch.empty(M, H, ops.DEC_SPLITS, 68, device=dev)
+                ops.attn_decode_split_qln_f32(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, cc,
+                                              cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, part, H=H, D=D,
+                                              row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
+                                              scale=scale, x_out=x1)
+                y2 = ops.linear_decode_merge_f32(part, L.ca_ow, L.ca_ob, M=M, residual=x1)
+            elif self._split_f32:  # 8 key slices per (row, head), merged by the out-projection
+                qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
                 part = torch.empty(M, H, ops.DEC_SPLITS, 68, device=dev)
                 ops.attn_decode_split_f32(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, part, H=H,
                                           D=D, row_stride=D, req_stride=cstride, head_stride=self.Smax * D,
                                           scale=scale)
                 y2 = ops.linear_decode_merge_f32(part, L.ca_ow, L.ca_ob, M=M, residual=x1)
             else:
+                qc = ops.linear_decode_ln(y1, L.n1[0], L.n1[1], L.cq_w, L.cq_b, x_out=x1)
                 oc = torch.empty(M, d, dtype=dt, device=dev)
                 ops.attn_decode(qc, cc, cc.view(-1)[H * self.Smax * D:], req_t, nkc_t, oc, H=H, D=D,
                                 row_stride=D, req_stride=cstride, head_stride=self.Smax * D, scale=scale)

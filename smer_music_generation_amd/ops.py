@@ -296,6 +296,17 @@ def attn_decode_split_f32(q, kcache, vcache, row_req, row_nkeys, part, *, H, D, 
          float(scale), _stream())
 
 
+def attn_decode_split_qln_f32(y, gamma, beta, wq, bq, kcache, vcache, row_req, row_nkeys, part, *, H, D,
+                              row_stride, req_stride, scale, head_stride=0, x_out=None, eps=1e-5):
+    """attn_decode_split_f32 whose query is LayerNorm(y) . wq^T + bq, both
+    computed in the attention blocks (fp32, d_model 512); x_out <- LayerNorm(y)."""
+    M, dm = y.shape
+    call("smer_attn_decode_split_qln_f32", M, H, D, _p(y), _ld(y), _p(gamma), _p(beta), float(eps), _p(wq),
+         _ld(wq), _p(bq), _p(x_out), _ld(x_out) if x_out is not None else 0, dm, _p(kcache), _p(vcache),
+         int(row_stride), int(req_stride), int(head_stride), _p(row_req), _p(row_nkeys), _p(part),
+         float(scale), _stream())
+
+
 def linear_decode_merge_f32(part, w, bias=None, *, M, residual=None, relu=False, out=None):
     """out = merge(part) @ w^T + bias (+relu) (+residual), fp32; merge()
     combines attn_decode_split_f32's slices into the attention output rows."""

@@ -1004,6 +1004,40 @@ def test_attn_decode_split_f32_merge(S, M):
     assert rel_err(got, ref) < 1e-5, rel_err(got, ref)
 
 
+@pytest.mark.parametrize("S,M", [(1100, 2), (40, 2), (2500, 4)])
+def test_attn_decode_split_qln_f32(S, M):
+    """fp32 split decode attention with LN + query projection in its blocks
+    == smer_linear_decode_ln_f32 (cross Q, x_out) -> split attention -> merge:
+    the stored LN output bit for bit (same normalisation arithmetic), the
+    merged output within fp32 reordering of the projection's sums; rows with
+    1 key (query skipped) and slices with no key."""
+    O = ops()
+    H, D, dm, R = 8, 64, 512, 3
+    cache = torch.randn(R, 2, H, S, D, device=dev)
+    y = torch.randn(M, dm, device=dev) * 2 + 0.5
+    g, be = torch.randn(dm, device=dev), torch.randn(dm, device=dev)
+    wq = torch.randn(dm, dm, device=dev) / math.sqrt(dm)
+    bq = torch.randn(dm, device=dev) * 0.1
+    req = torch.arange(M, device=dev, dtype=torch.int32) % R
+    nk = torch.tensor([S, 1, S // 3, 5][:M], device=dev, dtype=torch.int32)
+    kw = dict(H=H, D=D, row_stride=D, req_stride=2 * H * S * D, head_stride=S * D, scale=0.125)
+    w = torch.randn(dm, dm, device=dev) / math.sqrt(dm)
+    b = torch.randn(dm, device=dev)
+    xln = torch.empty_like(y)
+    q = O.linear_decode_ln(y, g, be, wq, bq, x_out=xln)
+    part = torch.empty(M, H, O.DEC_SPLITS, 68, device=dev)
+    O.attn_decode_split_f32(q, cache, cache.view(-1)[H * S * D:], req, nk, part, **kw)
+    ref = O.linear_decode_merge_f32(part, w, b, M=M, residual=xln)
+    x_out = torch.full_like(y, float("nan"))
+    part2 = torch.empty_like(part)
+    O.attn_decode_split_qln_f32(y, g, be, wq, bq, cache, cache.view(-1)[H * S * D:], req, nk, part2,
+                                x_out=x_out, **kw)
+    got = O.linear_decode_merge_f32(part2, w, b, M=M, residual=x_out)
+    torch.cuda.synchronize()
+    assert torch.equal(x_out, xln)
+    assert rel_err(got, ref) < 1e-5, rel_err(got, ref)
+
+
 # ------------------------------------------------------------ fp8
 def _e4m3_ref(x, amax):
     """e4m3 bytes of x * (448 / amax): f32 scale by IEEE division, f32
