@@ -2043,6 +2043,17 @@ static bool smer_gemm_glds_enabled() {
   return v == 1;
 }
 
+// SMER_WGRAD_GLDS=1: LDS-DMA staging for the 128x128 weight gradients too
+// (see launch_bf16; A/B and repeatability probes only)
+static bool smer_wgrad_glds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD_GLDS");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 // SMER_GEMM256=0 keeps every shape on the 128x128 kernel (A/B, tests).
 static bool smer_gemm256_enabled() {
   const char* e = getenv("SMER_GEMM256");  // read per call: A/B scripts flip it in-process
@@ -2100,13 +2111,17 @@ static int smer_splitk_depth() {
 // 16384; C4 step 90.1 vs 91.1 ms with every wgrad on it).  At C2's
 // 512-wide outputs the 128x128 kernel with its smaller split-K slabs is as
 // fast or faster.
-// SMER_WGRAD256=1 / 0 forces it on / off for every shape (A/B);
+// Round 5: every shape whose split-K fills the chip takes it (the 128x128
+// kernel now stages through registers, see launch_bf16: C2 13.66 vs 14.05 ms
+// with the 512-wide outputs on the register-staged 128 kernel).
+// SMER_WGRAD256=1 / 0 / 2 forces it on / off for every shape / the round-4
+// rule, outputs of at least 1536 x 768 (A/B);
 // SMER_WGRAD256_DEPTH: minimum K depth of its split-K slices
 static bool smer_wgrad256_enabled(int M, int N) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD256");
-    v = (e && e[0] == '1') ? 1 : (e && e[0] == '0') ? 0 : 2;
+    v = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
   }
   return v == 1 || (v == 2 && (long)M * N >= 1536L * 768);
 }
@@ -2364,8 +2379,14 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   const long nwg = (long)tiles * split;
   const long resident = split > 1 ? smer_wgrad_resident() : 2L * smer_num_cus();
   const int grid = nwg > resident ? (int)(resident & ~7L) : (int)nwg;
-  // LDS-DMA staging needs whole 64-deep K steps in every slice
-  const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled();
+  // LDS-DMA staging needs whole 64-deep K steps in every slice.  The weight
+  // gradients stage through registers unless SMER_WGRAD_GLDS=1: their
+  // LDS-DMA form, running on the side stream beside the dgrad chain, made
+  // whole train steps non-repeatable (bf16 C4: every gradient below the last
+  // decoder layer differed between identical steps; tools/grad_repeat.py),
+  // while each kernel alone is bit-exact
+  const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled() &&
+                  ((AK || BKC) || smer_wgrad_glds());
   if constexpr (!AK && !BKC) {
     // weight gradients at one resident workgroup per CU: the 3-stage ring
     const int ns = smer_wgrad_stages();
