@@ -44,6 +44,14 @@ def main():
                 rel = d.max().item() / max(ref[n].float().abs().max().item(), 1e-30)
                 nd = int((d > 0).sum().item())
                 bad.setdefault(n, []).append((k, nd, rel))
+    out = os.environ.get("SMER_GRAD_SAVE")
+    if out:  # the first step's gradients, for comparisons across processes / switches
+        torch.save({n: t.cpu() for n, t in ref.items()}, out)
+    cmp = os.environ.get("SMER_GRAD_CMP")
+    if cmp:
+        other = torch.load(cmp, weights_only=True)
+        diff = [n for n in names if not torch.equal(other[n], ref[n].cpu())]
+        print("vs %s: %d parameters differ (first: %s)" % (cmp, len(diff), diff[:3]))
     print("steps %d, parameters %d, differing %d" % (K, len(names), len(bad)))
     print("identical: %s" % [n for n in names if n not in bad])
     for n in names:
