@@ -2,7 +2,7 @@
 stepped K times at lr = 0 on the fixture batch (weights unchanged, no
 dropout), every step's gradients compared with the first; prints the
 parameters whose gradients differ and by how much.
-    python tools/grad_repeat.py [K] [precision]"""
+    python tools/grad_repeat.py [K] [precision] [c2bench]"""
 import os
 import sys
 
@@ -20,13 +20,24 @@ def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     prec = sys.argv[2] if len(sys.argv) > 2 else "bf16"
     dev = torch.device("cuda", 0)
-    z, meta = _fixture(os.path.join(ROOT, "tests", "golden"), "train_c4")
-    m = prod_model(C4, prec, z, meta["param_names"])
-    tr = Trainer(m, WordVocab(0, CTRL), lr=0.0, eos_weight=0.8)
-    src = z["src"].astype(np.int64)
-    tin = z["tgt_in"].astype(np.int64)
-    b = {"input": src, "target_in": tin, "target_out": z["tgt_out"].astype(np.int64),
-         "input_pad_mask": src == 0, "target_pad_mask": tin == 0}
+    if len(sys.argv) > 3 and sys.argv[3] == "c2bench":
+        # the bench's C2 step at full size (B 32, S 1024, T 256), dropout 0
+        import bench
+        from smer_music_generation_amd.synth import synth_training_batch
+        args = bench.parse_args([])
+        args.dropout = 0.0
+        m = bench.make_model(args, dev, prec)
+        v = WordVocab(0, CTRL)
+        tr = Trainer(m, v, lr=0.0)
+        b = synth_training_batch(1000, v, args.batch, args.seq, args.tgt)
+    else:
+        z, meta = _fixture(os.path.join(ROOT, "tests", "golden"), "train_c4")
+        m = prod_model(C4, prec, z, meta["param_names"])
+        tr = Trainer(m, WordVocab(0, CTRL), lr=0.0, eos_weight=0.8)
+        src = z["src"].astype(np.int64)
+        tin = z["tgt_in"].astype(np.int64)
+        b = {"input": src, "target_in": tin, "target_out": z["tgt_out"].astype(np.int64),
+             "input_pad_mask": src == 0, "target_pad_mask": tin == 0}
     bt = {k: torch.from_numpy(np.asarray(x)).to(dev) for k, x in b.items()}
     names = [n for n, _ in m.named_parameters()]
     ref = None
