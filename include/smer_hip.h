@@ -369,6 +369,12 @@ int smer_cast(int src_dtype, int dst_dtype, long n, const void* src, void* dst,
 /* strided 2-D copy with dtype conversion (dst[r*ldd+c] = src[r*lds+c]). */
 int smer_cast2d(int src_dtype, int dst_dtype, int rows, int cols, const void* src, long lds,
                 void* dst, long ldd, smer_stream_t stream);
+/* Debug: order-independent checksum of a strided region (rows x row_bytes,
+ * row stride ld_bytes, 4-byte words): out[0..nparts) receive partial sums
+ * of w_i * (2 i + 1) mod 2^64 that the caller adds (repeatability probes,
+ * tools/ck_log.py; not on the product path). */
+int smer_debug_checksum(const void* p, long rows, long row_bytes, long ld_bytes,
+                        unsigned long long* out, int nparts, smer_stream_t stream);
 size_t smer_colsum_workspace(int M, int N);
 /* out[n] (+)= sum_m x[m, n] (deterministic two-stage). */
 int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, int accumulate,

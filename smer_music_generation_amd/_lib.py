@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (must be imported before the HIP library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SMER_HIP_LIB", os.path.join(_HERE, "libsmer_hip.so"))
+LIB_PATH = os.environ.get("SMER_HIP_LIB") or os.path.join(_HERE, "libsmer_hip.so")
 
 c_int, c_long, c_float, c_size, c_u32 = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
                                          ctypes.c_size_t, ctypes.c_uint32)
@@ -115,6 +115,7 @@ SIGNATURES = {
     "smer_cast2d": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P]),
     "smer_colsum_workspace": (c_size, [c_int, c_int]),
     "smer_colsum": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, P, c_size, P]),
+    "smer_debug_checksum": (c_int, [P, c_long, c_long, c_long, P, c_int, P]),
 }
 
 _lib = None

@@ -33,9 +33,21 @@ def _hipcc():
     raise RuntimeError("hipcc not found (ROCm toolchain required to build libsmer_hip.so)")
 
 
+# No packed-FP32 VALU instructions (v_pk_fma_f32 / v_pk_mul_f32 /
+# v_pk_add_f32) anywhere in the library: on gfx950 their results came out
+# wrong in lanes 48-63 (one element of the register pair, a few ulps) while
+# a workgroup of another kernel streamed LDS-DMA (global_load_lds) on the
+# same CU -- the overlapped train step's LayerNorm backward beside the
+# 128x128 weight gradient on the side stream (DESIGN.md section 8,
+# tools/ck_log.py).  Without them every configuration repeats bit for bit,
+# and the step is faster (the packed ops were an anti-lever beside MFMAs
+# anyway).  tests/test_asm_hazards.py scans the built library for them.
+NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+
+
 def _flags():
     return ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH,
-            "-Wno-unused-result", "-I" + os.path.join(ROOT, "include")]
+            "-Wno-unused-result", "-I" + os.path.join(ROOT, "include")] + NO_PACKED_F32
 
 
 def _newer(target, deps):
@@ -45,10 +57,23 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
+def _flags_changed():
+    """True (and the stamp rewritten) when the compile flags differ from the
+    ones the objects under _build/ were built with."""
+    stamp = os.path.join(OBJ, "flags.txt")
+    cur = " ".join([_hipcc()] + _flags())
+    old = open(stamp).read() if os.path.exists(stamp) else None
+    if old != cur:
+        with open(stamp, "w") as f:
+            f.write(cur)
+        return True
+    return False
+
+
+def _compile(src, force=False):
     obj = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
     deps = [os.path.join(HERE, src)] + [os.path.join(HERE, h) for h in HEADERS]
-    if not _newer(obj, deps):
+    if not force and not _newer(obj, deps):
         return obj
     cmd = [_hipcc()] + _flags() + ["-c", os.path.join(HERE, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -78,9 +103,10 @@ def build_data(verbose=True):
 def build(verbose=True):
     build_data(verbose)
     os.makedirs(OBJ, exist_ok=True)
+    force = _flags_changed()
     jobs = min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, SOURCES))
+        objs = list(ex.map(lambda f: _compile(f, force), SOURCES))
     if _newer(OUT, objs):
         cmd = [_hipcc(), "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", OUT]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -2043,13 +2043,16 @@ static bool smer_gemm_glds_enabled() {
   return v == 1;
 }
 
-// SMER_WGRAD_GLDS=1: LDS-DMA staging for the 128x128 weight gradients too
-// (see launch_bf16; A/B and repeatability probes only)
+// SMER_WGRAD_GLDS=0: register staging for the 128x128 weight gradients
+// (round 5's workaround, see launch_bf16; A/B runs).  Default LDS-DMA since
+// round 6: the non-repeatable overlapped step was the packed-FP32 fault
+// (DESIGN.md section 8), not this kernel, and the library no longer
+// contains packed-FP32 instructions
 static bool smer_wgrad_glds() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD_GLDS");
-    v = (e && e[0] == '1') ? 1 : 0;
+    v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
 }
@@ -2111,19 +2114,21 @@ static int smer_splitk_depth() {
 // 16384; C4 step 90.1 vs 91.1 ms with every wgrad on it).  At C2's
 // 512-wide outputs the 128x128 kernel with its smaller split-K slabs is as
 // fast or faster.
-// Round 5: every shape whose split-K fills the chip takes it (the 128x128
-// kernel now stages through registers, see launch_bf16: C2 13.66 vs 14.05 ms
-// with the 512-wide outputs on the register-staged 128 kernel).
-// SMER_WGRAD256=1 / 0 / 2 forces it on / off for every shape / the round-4
-// rule, outputs of at least 1536 x 768 (A/B);
+// Round 5 sent every shape whose split-K fills the chip to it (the 128x128
+// kernel then staged through registers: C2 13.66 vs 14.05 ms).  Round 6,
+// with the 128x128 kernel on LDS-DMA again: outputs with both sides >= 768
+// (or >= 1536 x 768) take it -- every C4 weight gradient (C4 fp8 84.5-85.0
+// vs 85.6-86.3 ms with only the round-4 rule), no C2 one (C2 13.08-13.16 vs
+// 13.19-13.22 ms with all of them; tools/ab_step.py, interleaved rounds).
+// SMER_WGRAD256=2 (default) / 1 / 0: that rule / every shape / never (A/B);
 // SMER_WGRAD256_DEPTH: minimum K depth of its split-K slices
 static bool smer_wgrad256_enabled(int M, int N) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD256");
-    v = (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+    v = (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
   }
-  return v == 1 || (v == 2 && (long)M * N >= 1536L * 768);
+  return v == 1 || (v == 2 && ((long)M * N >= 1536L * 768 || (M >= 768 && N >= 768)));
 }
 // The 256x256 weight gradients on the staggered schedule
 // (gemm256s_wgrad_kernel; tools/bench_wgrad.py c4: 2304x768x65536 249 vs
@@ -2190,6 +2195,17 @@ static int smer_wgrad_stages() {
     v = e ? std::max(2, std::min(4, atoi(e))) : 2;
   }
   return v;
+}
+// SMER_WGRAD_LDS_PAD (bytes, repeatability probes only): extra dynamic LDS
+// requested by the LDS-DMA 128x128 weight gradient, so fewer other
+// workgroups share its CU (160 KiB in all: the CU to itself as far as LDS goes)
+static size_t smer_wgrad_lds_pad() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("SMER_WGRAD_LDS_PAD");
+    v = e ? std::max(0, std::min(96 * 1024, atoi(e))) : 0;
+  }
+  return (size_t)v;
 }
 static long smer_wgrad_resident() {
   static int v = -1;
@@ -2379,12 +2395,12 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   const long nwg = (long)tiles * split;
   const long resident = split > 1 ? smer_wgrad_resident() : 2L * smer_num_cus();
   const int grid = nwg > resident ? (int)(resident & ~7L) : (int)nwg;
-  // LDS-DMA staging needs whole 64-deep K steps in every slice.  The weight
-  // gradients stage through registers unless SMER_WGRAD_GLDS=1: their
-  // LDS-DMA form, running on the side stream beside the dgrad chain, made
-  // whole train steps non-repeatable (bf16 C4: every gradient below the last
-  // decoder layer differed between identical steps; tools/grad_repeat.py),
-  // while each kernel alone is bit-exact
+  // LDS-DMA staging needs whole 64-deep K steps in every slice.  (Round 5
+  // staged the weight gradients through registers because with LDS-DMA the
+  // overlapped step was not repeatable; round 6 traced that to packed-FP32
+  // VALU results corrupted beside LDS-DMA on the same CU, DESIGN.md section
+  // 8, and builds the library without them: SMER_WGRAD_GLDS=0 keeps the
+  // register form for A/B runs)
   const bool gl = (K % GBK) == 0 && (kchunk % GBK) == 0 && smer_gemm_glds_enabled() &&
                   ((AK || BKC) || smer_wgrad_glds());
   if constexpr (!AK && !BKC) {
@@ -2412,7 +2428,17 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
   }
   {
     auto kern = gl ? gemm_bf16_kernel<AK, BKC, true> : gemm_bf16_kernel<AK, BKC, false>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 4 * TILE_BYTES,
+    size_t lds = 4 * TILE_BYTES;
+    if (!AK && !BKC && gl && smer_wgrad_lds_pad()) {
+      lds += smer_wgrad_lds_pad();
+      static bool attr_pad = false;
+      if (!attr_pad) {
+        hipFuncSetAttribute((const void*)gemm_bf16_kernel<false, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_pad = true;
+      }
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds,
                        s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
                        (float*)ws, split > 1 ? rs_part : rowsum);
   }

@@ -322,3 +322,41 @@ extern "C" int smer_colsum(int dtype, int M, int N, const void* x, long ldx, flo
   SMER_CHECK_LAUNCH("smer_colsum");
   return SMER_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Debug checksum (repeatability probes, tools/ck_log.py): partial[b] =
+// sum over the 4-byte words w_i of a strided 2-D region of w_i * (2 i + 1)
+// (mod 2^64), word i = r * (row_bytes / 4) + c, block b taking every
+// nparts-th row.  The host adds the partials; the sum is order-independent,
+// so two runs over the same bits give the same value.  One launch on the
+// caller's stream, no allocation, no sync.
+__global__ __launch_bounds__(256) void checksum_kernel(const uint32_t* __restrict__ p, long rows,
+                                                       long row_words, long ld_words,
+                                                       unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long red[256];
+  unsigned long long a = 0;
+  for (long r = blockIdx.x; r < rows; r += gridDim.x) {
+    const uint32_t* row = p + r * ld_words;
+    const unsigned long long base = (unsigned long long)r * (unsigned long long)row_words;
+    for (long c = threadIdx.x; c < row_words; c += 256)
+      a += (unsigned long long)row[c] * (2ull * (base + (unsigned long long)c) + 1ull);
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+extern "C" int smer_debug_checksum(const void* p, long rows, long row_bytes, long ld_bytes,
+                                   unsigned long long* out, int nparts, smer_stream_t stream) {
+  SMER_REQUIRE(p && out, "smer_debug_checksum: null pointer");
+  SMER_REQUIRE(row_bytes % 4 == 0 && ld_bytes % 4 == 0 && ((uintptr_t)p & 3) == 0 && nparts > 0,
+               "smer_debug_checksum: 4-byte words only");
+  hipLaunchKernelGGL(checksum_kernel, dim3(nparts), dim3(256), 0, (hipStream_t)stream,
+                     (const uint32_t*)p, rows, row_bytes / 4, ld_bytes / 4, out);
+  SMER_CHECK_LAUNCH("smer_debug_checksum");
+  return SMER_OK;
+}

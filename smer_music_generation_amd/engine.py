@@ -429,6 +429,11 @@ class Engine:
         stream.wait_stream(torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(stream):
             ops.linear_wgrad(dy, x, gw, ws=ws, **kw)
+            if ops.CK_LOG is not None:
+                ops.ck("S:dW", gw)
+                ops.ck("S:db", kw.get("db"))
+                ops.ck("S:dy", dy)
+                ops.ck("S:x", x)
         # temporaries freed on the main stream must not be reused before the
         # side stream has read them
         dy.record_stream(stream)
@@ -482,6 +487,11 @@ class Engine:
                       dbeta=gw[1], param_stream=ps)
             if f8 is None:
                 ops.layernorm_bwd(g_in, y_, mu, rs, wb[0], dx_, **kw)
+                if ops.CK_LOG is not None:
+                    ops.ck("M:ln_in.g", g_in)
+                    ops.ck("M:ln_in.y", y_)
+                    ops.ck("M:ln_in.mu", mu)
+                    ops.ck("M:ln_in.rs", rs)
                 return None
             si = f8.site(site)
             q = torch.empty(y_.shape, dtype=torch.uint8, device=dev)
@@ -528,13 +538,17 @@ class Engine:
         side = self._wgrad_stream(dev, dt)
         ps = side[0] if side is not None else None  # LayerNorm dgamma / dbeta reductions too
         wg = lambda *a, **kw: self._wgrad(side, *a, **kw)  # noqa: E731
+        ops.ck("M:dlog", dlog_pad)
         wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
+        ck = ops.ck
+        ck("M:g_out", g_out)
         # final decoder norm
         y_last, mo, ro = ctx.dec_last
         dy = torch.empty_like(y_last)
         ops.layernorm_bwd(g_out, y_last, mo, ro, W.dec_norm[0], dy, dgamma=G.dec_norm[0],
                           dbeta=G.dec_norm[1], param_stream=ps)
+        ck("M:dy_final", dy)
         if hook:
             self._hook(side, hook, "head")
         # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
@@ -553,17 +567,22 @@ class Engine:
             dy3 = torch.empty_like(y3)
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
+            ck("M:dec%d.dy3" % i, dy3d)
             wg(dy3d, h, GL.l2_w, db=GL.l2_b)
             dh, dhq = dgrad(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, q_site="b.dec%d.dh" % i, gate=h,
                             gate_scale=ops.drop_scale(p_tr))
+            ck("M:dec%d.dh" % i, dh)
             wg(dh, x2, GL.l1_w, db=GL.l1_b)
             dx2, _ = dgrad(dhq, dh, "dec%d.l1" % i, L.l1_w, residual=dy3)
+            ck("M:dec%d.dx2" % i, dx2)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx2, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("dec", i, 3)), GL.n2, "b.dec%d.ln2" % i)
+            ck("M:dec%d.dy2" % i, dy2d)
             wg(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
             doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
+            ck("M:dec%d.doc" % i, doc)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
             dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
             q8c, dqcq = None, None
@@ -578,23 +597,30 @@ class Engine:
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)),
                          q8=q8c)
+            ck("M:dec%d.dqc" % i, dqc)
+            ck("M:dec%d.dkvc" % i, dkvc)
             wg(dqc, x1, GL.cq_w, db=GL.cq_b)
             wg(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
             dx1, _ = dgrad(dqcq, dqc, "dec%d.cq" % i, L.cq_w, residual=dy2)
+            ck("M:dec%d.dx1" % i, dx1)
             # self-attention block
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("dec", i, 1)), GL.n1, "b.dec%d.ln1" % i)
+            ck("M:dec%d.dy1" % i, dy1d)
             wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
             do, _ = dgrad(dy1q, dy1d, "dec%d.sao" % i, L.sa_ow)
+            ck("M:dec%d.do" % i, do)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
             q8s, dqkvq = attn_q8((Mt, 3 * d), "b.dec%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
                          seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)), q8=q8s)
+            ck("M:dec%d.dqkv" % i, dqkv)
             wg(dqkv, y_in, GL.sa_w, db=GL.sa_b)
             dy, _ = dgrad(dqkvq, dqkv, "dec%d.sa" % i, L.sa_w, residual=dy1)
+            ck("M:dec%d.dy" % i, dy)
             if hook:
                 self._hook(side, hook, "dec%d" % i)
         d_tgt = dy
@@ -608,6 +634,7 @@ class Engine:
                 dmem = ops.linear_dgrad(dkvc_all, W.ckv_all, out_f32=torch.empty(Ms, d, device=dev))
         else:
             dmem = torch.zeros(Ms, d, device=dev)
+        ck("M:dmem", dmem)
         # encoder
         x_last, me, re = ctx.enc_last
         dx = torch.empty_like(x_last)
@@ -619,24 +646,31 @@ class Engine:
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
+            ck("M:enc%d.dy2" % i, dy2d)
             wg(dy2d, h, GL.l2_w, db=GL.l2_b)
             dh, dhq = dgrad(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, q_site="b.enc%d.dh" % i, gate=h,
                             gate_scale=ops.drop_scale(p_tr))
+            ck("M:enc%d.dh" % i, dh)
             wg(dh, x1, GL.l1_w, db=GL.l1_b)
             dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)
+            ck("M:enc%d.dx1" % i, dx1)
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("enc", i, 1)), GL.n1, "b.enc%d.ln1" % i)
+            ck("M:enc%d.dy1" % i, dy1d)
             wg(dy1d, o, GL.out_w, db=GL.out_b)
             do, _ = dgrad(dy1q, dy1d, "enc%d.out" % i, L.out_w)
+            ck("M:enc%d.do" % i, do)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
             q8s, dqkvq = attn_q8((Ms, 3 * d), "b.enc%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
             ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
                          dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
                          seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)), q8=q8s)
+            ck("M:enc%d.dqkv" % i, dqkv)
             wg(dqkv, x_in, GL.in_w, db=GL.in_b)
             dx, _ = dgrad(dqkvq, dqkv, "enc%d.in" % i, L.in_w, residual=dy1)
+            ck("M:enc%d.dx" % i, dx)
             if hook:
                 self._hook(side, hook, "enc%d" % i)
         # shared embedding (model.py:76): both streams scatter into one table

@@ -561,6 +561,26 @@ def clear_decode_sessions(model=None):
         del _BATCH_SESSIONS[key]
 
 
+def _plugin_capacity(Smax, Tmax):
+    """Capacities of a warm batch-1 (plugin) session: rounded up to powers of
+    two (>= 128), so consecutive calls on sources / mask counts of similar
+    size reuse one session and its captured graphs instead of rebuilding
+    them (a rebuild + capture costs ~6 ms, 1/4 of a typical call); a fresh
+    session for the same request rounds the same way.  The rounding never
+    carries a capacity across 512 rows, where the decode attention switches
+    to its 8-wave variant (another summation order), so warm and cold
+    sessions give the same logits.  Tmax excludes the trash slot (the cache
+    holds Tmax + 1 rows)."""
+    S0, T0 = int(Smax), int(Tmax)
+    S = 1 << max(7, (S0 - 1).bit_length())
+    if S0 < 512:
+        S = min(S, 511)
+    T = (1 << max(7, T0.bit_length())) - 1
+    if T0 + 1 < 512:
+        T = min(T, 510)
+    return S, T
+
+
 def _batch_session(model, R, Smax, Tmax, precision, exact_tmax=False, warm=True):
     """A decode session for this call.  A cached one is reused only when it
     still addresses the model's current weight buffers (moving the model
@@ -575,13 +595,7 @@ def _batch_session(model, R, Smax, Tmax, precision, exact_tmax=False, warm=True)
     if not warm:
         return DecodeSession(model, R, Smax, Tmax)
     if R == 1 and not exact_tmax:
-        # the plugin call: capacities rounded up to powers of two (>= 128), so
-        # consecutive calls on sources / mask counts of similar size reuse one
-        # session and its captured graphs instead of rebuilding them (a
-        # rebuild + capture costs ~6 ms, 1/4 of a typical call); a fresh
-        # session for the same request rounds the same way
-        Smax = 1 << max(7, (int(Smax) - 1).bit_length())
-        Tmax = (1 << max(7, int(Tmax).bit_length())) - 1
+        Smax, Tmax = _plugin_capacity(Smax, Tmax)
     key = (id(model), model.precision, R)
     s = _BATCH_SESSIONS.get(key)
     fits = (s is not None and s.model is model and s.Smax >= Smax and s.Tmax >= Tmax + 1

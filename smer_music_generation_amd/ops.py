@@ -100,6 +100,55 @@ def gemm(A, B, *, M, N, K, a_kcontig=True, b_kcontig=True, out=None, out_f32=Non
         timer.records.append((ev0, ev1, 2.0 * M * N * K, tag))
 
 
+class CkLog:
+    """Repeatability probe (tools/ck_log.py): an order-independent checksum
+    of a tensor taken on the current stream into a preallocated device log,
+    no host sync, no allocation per entry.  Engine.backward calls `ck()` after
+    each launch when `ops.CK_LOG` is set; not used on the product path."""
+
+    PARTS = 64
+
+    def __init__(self, device, n=4096, keep=()):
+        self.buf = torch.zeros(n * self.PARTS, dtype=torch.int64, device=device)
+        self.n = n
+        self.names = []
+        self.keep = tuple(keep)  # name substrings whose tensors are also cloned
+        self.kept = {}
+
+    def add(self, name, t):
+        i = len(self.names)
+        if i >= self.n:
+            return
+        if t.dim() == 1:
+            rows, row_b, ld_b = 1, t.numel() * t.element_size(), t.numel() * t.element_size()
+        else:
+            t2 = t.reshape(-1, t.shape[-1]) if t.dim() > 2 else t
+            rows, row_b, ld_b = t2.shape[0], t2.shape[1] * t2.element_size(), _ld(t2) * t2.element_size()
+        self.names.append((name, torch.cuda.current_stream(t.device).cuda_stream))
+        call("smer_debug_checksum", _p(t), rows, row_b, ld_b, self.buf.data_ptr() + i * self.PARTS * 8,
+             self.PARTS, _stream())
+        if any(k in name for k in self.keep):
+            self.kept[i] = t.clone()
+
+    def values(self):
+        import numpy as np
+        v = self.buf.view(self.n, self.PARTS)[:len(self.names)].cpu().numpy().view(np.uint64)
+        return [int(x) for x in v.sum(axis=1, dtype=np.uint64)]
+
+    def reset(self):
+        self.buf.zero_()
+        self.names = []
+        self.kept = {}
+
+
+CK_LOG = None
+
+
+def ck(name, t):
+    if CK_LOG is not None and t is not None:
+        CK_LOG.add(name, t)
+
+
 _SPLITK_WS = {}
 SPLITK_WS_BYTES = 64 << 20
 

@@ -64,9 +64,27 @@ def test_gemm_kernels_have_no_early_reads(tmp_path):
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     src = os.path.join(ROOT, "smer_music_generation_amd", "csrc", "gemm.hip")
     out = tmp_path / "gemm.s"
+    from smer_music_generation_amd.csrc.build import NO_PACKED_F32
     r = subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                        "-I" + os.path.join(ROOT, "include"), src, "-o", str(out)],
+                        "-I" + os.path.join(ROOT, "include"), src, "-o", str(out)] + NO_PACKED_F32,
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     bad = {f: v for f, v in check(str(out)).items() if "gemm" in f}
     assert not bad, bad
+
+
+def test_library_has_no_packed_f32_instructions():
+    """DESIGN.md section 8 (round 6): packed-FP32 VALU results (v_pk_fma_f32 /
+    v_pk_mul_f32 / v_pk_add_f32) came out wrong in lanes 48-63 while another
+    workgroup on the same CU streamed LDS-DMA, which made the overlapped
+    train step non-repeatable.  The library is built without them
+    (csrc/build.py NO_PACKED_F32); this scans the shipped gfx950 code."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pk_scan
+    lib = os.path.join(ROOT, "smer_music_generation_amd", "libsmer_hip.so")
+    if not os.path.exists(lib) or not pk_scan.tools_available():
+        pytest.skip("built library or LLVM tools absent")
+    n, found = pk_scan.scan(lib)
+    assert n >= 5, "expected the gfx950 code objects of every .hip source, found %d" % n
+    assert not found, "packed-FP32 instructions in %s" % sorted(found.items(), key=lambda x: -x[1])[:5]

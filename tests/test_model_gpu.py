@@ -594,3 +594,27 @@ def test_device_sampler_draws_match_numpy_on_random_rows():
     mth = mt.cpu().numpy().view(np.uint32)
     assert dev_ids == host
     assert int(mth[624]) == st_host[2] and np.array_equal(mth[:624], st_host[1])
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_plugin_warm_equals_cold_below_512_rows(golden_dir, precision):
+    """a batch-1 request with 3 masked bars and a source
+    of ~300 tokens (raw capacities 257-511 rows) decodes to the same ids on
+    the warm (power-of-two rounded) session as on a cold one; both stay in
+    the decode attention's < 512-row variant class."""
+    from smer_music_generation_amd import generation as G
+    from smer_music_generation_amd.synth import synth_events
+    from smer_music_generation_amd.vocab import WordVocab
+    z, meta = _golden(golden_dir)
+    m = _model(z, meta, precision)
+    v = WordVocab(0, CTRL)
+    ctl = _infill_cases(golden_dir)["all_controls"]
+    ev = synth_events(123, n_bars=7, n_tracks=2)  # 333 events
+    req = [(list(ev), [1], [1, 2, 3])]
+    G.clear_decode_sessions()
+    warm = G.generation_batch(m, [(list(e), t, b) for e, t, b in req], v, ctl, greedy=True)
+    sess = next(iter(G._BATCH_SESSIONS.values()))
+    assert sess.Smax < 512 and sess.Tmax < 512, (sess.Smax, sess.Tmax)
+    cold = G.generation_batch(m, [(list(e), t, b) for e, t, b in req], v, ctl, greedy=True, warm=False)
+    assert [None if x is None else ([str(t) for t in x[0]], x[1:]) for x in warm] == \
+        [None if x is None else ([str(t) for t in x[0]], x[1:]) for x in cold]

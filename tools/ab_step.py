@@ -1,6 +1,7 @@
 """A/B of one environment switch on the train step: each value in its own
 process (the switches are read once per process), rounds interleaved.
-    python tools/ab_step.py c2|c4|c4bf16 ENV_NAME VALUE_A VALUE_B ... [--rounds 2]"""
+    python tools/ab_step.py c2|c4|c4bf16 ENV_NAME VALUE_A VALUE_B ... [--rounds 2]
+    python tools/ab_step.py c2 ENV "A=1,B=2" "A=0" ...   (several switches per value)"""
 import json
 import os
 import subprocess
@@ -17,7 +18,13 @@ res = {v: [] for v in values}
 for r in range(rounds):
     for v in values:
         env = dict(os.environ)
-        env[name] = v
+        if name == "ENV":
+            for kv in v.split(","):
+                if kv:
+                    k, x = kv.split("=", 1)
+                    env[k] = x
+        else:
+            env[name] = v
         if cfg == "c2":
             cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "3",
                    "--no-infill", "--no-cpu", "--no-c4", "--no-c5", "--no-roofline"]
