@@ -80,7 +80,7 @@ __device__ bool grammar_commit(int r, int idx, bool fail, int flags, int len, in
   st[ST_LEN] = nlen;
   st[ST_FLAGS] = f;
   if (!done && pos + nf > trash_pos) {  // decoder prefix would overrun the cache
-    st[ST_ERR] = 1;
+    st[ST_ERR] |= 1;
     done = true;
   }
   // next step's rows 2r (first) and 2r+1 (last): dummies unless fed

@@ -494,6 +494,8 @@ class DecodeSession:
         stream continues exactly as if the host had drawn.  Returns
         (per-request emitted ids, steps, error flags, per-request redraw
         failure flags)."""
+        if all(sp.done for sp in spans):  # nothing to draw: np.random stays untouched
+            return [[] for _ in spans], 0, np.zeros(len(spans), dtype=np.int32), [[] for _ in spans]
         st0 = np.random.get_state()
         if st0[0] != "MT19937":
             raise RuntimeError("sampled_decode: np.random is not MT19937")
@@ -559,6 +561,8 @@ class DecodeSession:
             mt_t = torch.from_numpy(sample[1].view(np.int32))
             if getattr(self, "g_mt", None) is None:
                 self.g_mt = torch.zeros(625, dtype=torch.int32, device=dev)
+            if getattr(self, "g_reject", None) is None or tuple(self.g_reject.shape) != tuple(keep.shape):
+                # (a captured graph keyed on another keep shape is never replayed for this one)
                 self.g_reject = torch.zeros(keep.shape, dtype=torch.uint8, device=dev)
             self.g_mt.copy_(mt_t)
             self.g_reject.copy_(reject_t)

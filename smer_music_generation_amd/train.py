@@ -226,10 +226,14 @@ class Trainer:
     group when torch.distributed is initialised (world_size > 1)."""
 
     def __init__(self, model, vocab, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, eos_weight=0.8,
-                 group=None, grad_wire_dtype=None, broadcast=True):
+                 group=None, grad_wire_dtype=None, broadcast=True, dp=None):
         """grad_wire_dtype: None / torch.float32 (default, parity) or
         torch.bfloat16 for the DP gradient all-reduce (see GradBucketer).
-        broadcast: under DP, copy rank 0's parameters to every rank here."""
+        broadcast: under DP, copy rank 0's parameters to every rank here.
+        dp: run the data-parallel path (normaliser all-reduce, per-layer
+        bucketed gradient all-reduces issued from the backward hooks) --
+        default: when the process group has more than one rank; True also
+        at world size 1 (the real RCCL calls and stream ordering on one GPU)."""
         self.model = model
         self.vocab = vocab
         dev = model.flat_parameters().device
@@ -243,11 +247,14 @@ class Trainer:
         self.optimizer = FusedAdam(model, self.m, self.v, lr, betas, eps)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        if dp and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("Trainer(dp=True) needs an initialised torch.distributed process group")
+        self.dp = self.world > 1 if dp is None else bool(dp)
         self._ranges = layer_ranges(model)
         self._seed = 1
         self.grad_wire_dtype = grad_wire_dtype
         self._bucketer = None
-        if self.world > 1 and broadcast:
+        if self.dp and broadcast:
             broadcast_parameters(model, group)
 
     # hyper-parameters live in the optimizer's param group (schedulers edit it)
@@ -301,7 +308,7 @@ class Trainer:
         y = tout.reshape(-1).contiguous().long()
         denom = torch.empty(1, device=logits.device)
         ops.wce_denom(y, self.ce_all, denom)
-        if self.world > 1:
+        if self.dp:
             dist.all_reduce(denom, group=self.group)
         dlog = torch.zeros(B * T, eng.Vp, dtype=ctx.dt, device=logits.device)
         row_loss = torch.empty(B * T, device=logits.device)
@@ -311,7 +318,7 @@ class Trainer:
         grad.zero_()
         hook = None
         bucketer = None
-        if self.world > 1:
+        if self.dp:
             if self._bucketer is None or self._bucketer.flat is not grad:
                 # persistent: the bf16 shadow is allocated once
                 self._bucketer = GradBucketer(grad, self._ranges, self.group,

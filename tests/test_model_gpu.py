@@ -598,8 +598,8 @@ def test_device_sampler_draws_match_numpy_on_random_rows():
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_plugin_warm_equals_cold_below_512_rows(golden_dir, precision):
-    """a batch-1 request with 3 masked bars and a source
-    of ~300 tokens (raw capacities 257-511 rows) decodes to the same ids on
+    """a batch-1 request with 5 masks and a source of
+    ~300 tokens (raw capacities 257-511 rows) decodes to the same ids on
     the warm (power-of-two rounded) session as on a cold one; both stay in
     the decode attention's < 512-row variant class."""
     from smer_music_generation_amd import generation as G
@@ -609,8 +609,8 @@ def test_plugin_warm_equals_cold_below_512_rows(golden_dir, precision):
     m = _model(z, meta, precision)
     v = WordVocab(0, CTRL)
     ctl = _infill_cases(golden_dir)["all_controls"]
-    ev = synth_events(123, n_bars=7, n_tracks=2)  # 333 events
-    req = [(list(ev), [1], [1, 2, 3])]
+    ev = synth_events(123, n_bars=7, n_tracks=2)
+    req = [(list(ev), [1], [2])]  # a 322-token source with 5 masks: raw capacities 322 / 509 rows
     G.clear_decode_sessions()
     warm = G.generation_batch(m, [(list(e), t, b) for e, t, b in req], v, ctl, greedy=True)
     sess = next(iter(G._BATCH_SESSIONS.values()))
