@@ -88,7 +88,10 @@ const char* smer_last_error(void);
  *   accumulate=1 adds into Cf).  bf16 path: MFMA 16x16x32; f32 path: VALU.
  * workspace (nullable, 16-B aligned): lets a Cf-only GEMM with few output
  *   tiles and a long K (weight gradients) split K into deterministic fp32
- *   slabs of M*N floats each, summed in fixed order by a second kernel. */
+ *   slabs of M*N floats each, summed in fixed slice order by the tile's
+ *   last-arriving slice (or a second kernel).  Its last 64 KiB hold per-tile
+ *   tickets: they must be ZERO when the workspace is first used (allocate
+ *   it zeroed); every call leaves them zero.  One workspace per stream. */
 int smer_gemm(int dtype, int a_kcontig, int b_kcontig, int M, int N, int K,
               const void* A, long lda, const void* B, long ldb,
               const float* bias, float alpha, int relu,

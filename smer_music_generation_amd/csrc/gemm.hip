@@ -231,6 +231,92 @@ __device__ __forceinline__ bf16x8 frag(const char* buf, int rbase, int s, int la
 }
 }  // namespace
 
+// Split-K hand-off for the fused (last-arriver) reduction: every slab /
+// row-sum partial byte is stored write-through (`sc1`) and read back with
+// `sc1` loads, each storing wave waits vmcnt(0), a workgroup barrier, then
+// ONE lane adds to the tile's ticket (agent-scope atomic); the workgroup
+// whose add returns ksplit - 1 sums the slices.  This is the first row of
+// the hand-off table in MI355X_MICROARCH.md (Valid forms): no release /
+// acquire fences needed.  The ticket is reset by the last arriver, so the
+// ticket words stay zero between launches.
+__device__ __forceinline__ void st_sc1_x4(float* p, float a, float b, float c, float d) {
+  const f32x4 v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ld_sc1_x4(const float* p) {
+  f32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void ld_sc1_retire(f32x4 (&b)[N]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(b[i]));
+}
+
+// The last arriver's reduction of one 128x128 tile: Cf (+)= alpha * sum of
+// the ksplit slabs in slice order (the splitk_reduce_kernel arithmetic), and
+// for tn == 0 tiles the bias row sums (+)= alpha * sum of the partials.
+// Needs N % 4 == 0, ldcf % 4 == 0 and a 16-B aligned Cf (launcher checks).
+__device__ __forceinline__ void splitk_tile_reduce(const GemmEpi& e, int M, int N, int m0, int n0,
+                                                   int ksplit, const float* __restrict__ slabs,
+                                                   const float* __restrict__ rs_part,
+                                                   float* __restrict__ rs_final, bool rs_tile,
+                                                   int tid) {
+  const long MN = (long)M * N;
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {  // 8 float4 per thread per pass, all in flight
+    f32x4 a[8], b[8];
+    long off[8];
+    bool ok[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pos = tid + 256 * (half * 8 + i);
+      const int row = pos >> 5, c4 = pos & 31;
+      const int grow = m0 + row, gcol = n0 + c4 * 4;
+      ok[i] = grow < M && gcol < N;
+      off[i] = ok[i] ? (long)grow * N + gcol : 0;  // clamped: discarded below
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = ld_sc1_x4(slabs + off[i]);
+    ld_sc1_retire(a);
+#pragma unroll 1
+    for (int sl = 1; sl < ksplit; ++sl) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = ld_sc1_x4(slabs + (long)sl * MN + off[i]);
+      ld_sc1_retire(b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a[i][0] += b[i][0]; a[i][1] += b[i][1]; a[i][2] += b[i][2]; a[i][3] += b[i][3];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (!ok[i]) continue;
+      const int pos = tid + 256 * (half * 8 + i);
+      const int row = pos >> 5, c4 = pos & 31;
+      float* p = e.Cf + (long)(m0 + row) * e.ldcf + n0 + c4 * 4;
+      float4 o = make_float4(a[i][0] * e.alpha, a[i][1] * e.alpha, a[i][2] * e.alpha, a[i][3] * e.alpha);
+      if (e.accumulate) {
+        const float4 c = *reinterpret_cast<const float4*>(p);
+        o.x = c.x + o.x; o.y = c.y + o.y; o.z = c.z + o.z; o.w = c.w + o.w;
+      }
+      *reinterpret_cast<float4*>(p) = o;
+    }
+  }
+  if (rs_tile && tid < GBM && m0 + tid < M) {
+    const int m = m0 + tid;
+    float t = 0.f;
+    for (int sl = 0; sl < ksplit; ++sl)
+      t += __hip_atomic_load(rs_part + (long)sl * M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    rs_final[m] = (e.rs_accumulate ? rs_final[m] : 0.f) + e.alpha * t;
+  }
+}
+
 // NSTG = 3 / 4 (weight gradients, LDS-DMA, one workgroup per CU): an
 // NSTG-stage LDS ring, each k-step's tiles requested NSTG - 1 steps ahead and
 // waited with a counted vmcnt before a raw barrier (the 2-stage form waits at the end of
@@ -243,11 +329,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
                                                            const bf16* __restrict__ B, long ldb,
                                                            GemmEpi e, int ksplit, int kchunk,
                                                            float* __restrict__ slabs,
-                                                           float* __restrict__ rowsum) {
+                                                           float* __restrict__ rowsum,
+                                                           unsigned* __restrict__ tickets = nullptr,
+                                                           float* __restrict__ rs_final = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int nbm = (M + GBM - 1) / GBM, nbn = (N + GBN - 1) / GBN;
+  // fused split-K reduction (tickets): slabs / partials stored write-through
+  const bool fused = tickets != nullptr && ksplit > 1;
   const int ntiles = nbm * nbn;
   const int nwg = ntiles * ksplit;
   // Persistent, XCD-aware work list: XCD x (blocks b with b % 8 == x) owns a
@@ -440,7 +530,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         for (int r = 0; r < 4; ++r) {
           const int row = m0 + wm * 64 + (2 * wn + j) * 16 + 4 * (lane >> 4) + r;
           if (row < M) {
-            if (ksplit > 1) rowsum[(long)it.split * M + row] = accr[j][r];
+            if (fused) st_sc1(rowsum + (long)it.split * M + row, accr[j][r]);
+            else if (ksplit > 1) rowsum[(long)it.split * M + row] = accr[j][r];
             else rowsum[row] = (e.rs_accumulate ? rowsum[row] : 0.f) + accr[j][r] * e.alpha;
           }
         }
@@ -478,7 +569,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
           if (slab) {
             const int valid = min(8, N - gcol);
             float* dst = slab + (long)grow * N + gcol;
-            if (valid == 8 && (N & 3) == 0) {
+            if (fused) {  // N % 4 == 0 (launcher): whole float4 pieces
+              st_sc1_x4(dst, v[0], v[1], v[2], v[3]);
+              if (valid > 4) st_sc1_x4(dst + 4, v[4], v[5], v[6], v[7]);
+            } else if (valid == 8 && (N & 3) == 0) {
               *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
               *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
             } else {
@@ -490,6 +584,25 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(int M, int N, int K,
         }
       }
       __syncthreads();
+    }
+    if (fused) {
+      // every wave's slab / partial stores done, then ONE lane takes the
+      // tile's ticket; the slice that arrives last sums all of them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int tile = it.tm * nbn + it.tn;
+        const unsigned old = __hip_atomic_fetch_add(tickets + tile, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == (unsigned)(ksplit - 1);
+        if (last) __hip_atomic_store(tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<volatile int*>(smem) = last;  // the epilogue tile is dead here
+      }
+      __syncthreads();
+      if (*reinterpret_cast<volatile int*>(smem))
+        splitk_tile_reduce(e, M, N, m0, n0, ksplit, slabs, rowsum, rs_final,
+                           rowsum != nullptr && it.tn == 0, tid);
+      __syncthreads();  // the flag word is overwritten by the next item's staging
     }
   }
 }
@@ -2227,6 +2340,26 @@ static long smer_g256_min_tiles() {
   return v;
 }
 
+// Split-K tickets (fused last-arriver reduction): the LAST SPLITK_TICKET_BYTES
+// of a split-K workspace hold one u32 per output tile.  They must be zero
+// when the workspace is first used (callers allocate it zeroed); every
+// launch leaves them zero (the last arriver resets its tile's ticket).
+constexpr size_t SPLITK_TICKET_BYTES = 64 * 1024;
+// SMER_SPLITK_FUSED=1: the fused last-arriver reduction instead of the
+// separate splitk_reduce_kernel (read per call).  Off by default: C2 step
+// 13.64-16.62 ms fused vs 13.04-13.09 separate (three interleaved rounds,
+// tools/ab_step.py, round 6) -- every slice waits for its 64 KiB of
+// write-through slab stores before taking the ticket, and the last arriver
+// sums the tile alone, both stalls of the persistent weight-gradient
+// workgroups; bit-identical either way
+static bool smer_splitk_fused() {
+  const char* e = getenv("SMER_SPLITK_FUSED");
+  return e && e[0] == '1';
+}
+static size_t splitk_slab_bytes(size_t ws_bytes) {
+  return ws_bytes > SPLITK_TICKET_BYTES ? ws_bytes - SPLITK_TICKET_BYTES : 0;
+}
+
 static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) {
   bool cf_only = e.Cf && !e.C && !e.bias && !e.residual && !e.gate && !e.relu && !e.drop_thr;
   if (!cf_only) return 1;
@@ -2238,7 +2371,7 @@ static int choose_split(int M, int N, int K, const GemmEpi& e, size_t ws_bytes) 
   long s = smer_wgrad_resident() / tiles;
   s = std::min<long>(s, K / smer_splitk_depth());
   // slabs of M*N floats plus M floats of row-sum partials per K slice
-  s = std::min<long>(s, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
+  s = std::min<long>(s, (long)(splitk_slab_bytes(ws_bytes) / (((size_t)M * N + M) * sizeof(float))));
   s = std::max<long>(1, std::min<long>(s, 64));
   return (int)s;
 }
@@ -2335,7 +2468,7 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     const long t2 = (long)((M + G2 - 1) / G2) * ((N + G2 - 1) / G2);
     const long cus = smer_num_cus();
     long ns = std::min<long>(smer_wgrad256_slots() / std::max<long>(1, t2), K / smer_wgrad256_depth());
-    ns = std::min<long>(ns, (long)(ws_bytes / (((size_t)M * N + M) * sizeof(float))));
+    ns = std::min<long>(ns, (long)(splitk_slab_bytes(ws_bytes) / (((size_t)M * N + M) * sizeof(float))));
     ns = std::max<long>(1, std::min<long>(ns, 64));
     if (cf_only && t2 * ns * 4 >= 3 * cus) {
       int kchunk = (int)(((K + ns - 1) / ns + G2K - 1) / G2K * G2K);
@@ -2390,6 +2523,13 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     split = (K + kchunk - 1) / kchunk;
   }
   float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
+  // fused split-K reduction by the tile's last-arriving slice (no separate
+  // reduce launch): whole float4 rows of dW
+  unsigned* tickets = nullptr;
+  if (split > 1 && smer_splitk_fused() && (N & 3) == 0 && (e.ldcf & 3) == 0 &&
+      ((uintptr_t)e.Cf & 15) == 0 && (size_t)tiles * 4 <= SPLITK_TICKET_BYTES &&
+      ws_bytes >= SPLITK_TICKET_BYTES)
+    tickets = (unsigned*)((char*)ws + ws_bytes - SPLITK_TICKET_BYTES);
   // persistent grid: two resident workgroups per CU (LDS 64 KiB, <= 256 VGPRs);
   // split-K weight gradients: smer_wgrad_resident()
   const long nwg = (long)tiles * split;
@@ -2418,11 +2558,11 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       if (ns == 4)
         hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, 4>), dim3(grid), dim3(256), 8 * TILE_BYTES, s,
                            M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
-                           rs_part);
+                           rs_part, tickets, rowsum);
       else
         hipLaunchKernelGGL((gemm_bf16_kernel<false, false, true, 3>), dim3(grid), dim3(256), 6 * TILE_BYTES, s,
                            M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk, (float*)ws,
-                           rs_part);
+                           rs_part, tickets, rowsum);
       goto reduce;
     }
   }
@@ -2440,10 +2580,10 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds,
                        s, M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e, split, kchunk,
-                       (float*)ws, split > 1 ? rs_part : rowsum);
+                       (float*)ws, split > 1 ? rs_part : rowsum, tickets, rowsum);
   }
 reduce:
-  if (split > 1) {
+  if (split > 1 && !tickets) {
     long n4 = ((long)M * N) / 4 + (rowsum ? M : 0);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,
                        (const float*)ws, e.alpha, e.Cf, e.ldcf, e.accumulate,

@@ -416,7 +416,7 @@ class Engine:
         side = self._side.get(dev)
         if side is None:
             side = (torch.cuda.Stream(device=dev),
-                    torch.empty(ops.SPLITK_WS_BYTES, dtype=torch.uint8, device=dev))
+                    torch.zeros(ops.SPLITK_WS_BYTES, dtype=torch.uint8, device=dev))  # zero split-K tickets
             self._side[dev] = side
         return side
 

@@ -157,7 +157,7 @@ def splitk_workspace(device):
     """Persistent per-device split-K slab buffer (stream-ordered reuse)."""
     ws = _SPLITK_WS.get(device)
     if ws is None:
-        ws = torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+        ws = torch.zeros(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)  # its tail: split-K tickets, zero
         _SPLITK_WS[device] = ws
     return ws
 

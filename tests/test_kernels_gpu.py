@@ -111,6 +111,36 @@ def test_gemm_wgrad_bias(M, N, K, acc):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,N,K,acc", [(512, 512, 32768, True), (1536, 512, 8192, False),
+                                       (309, 512, 4096, True), (2048, 512, 32768, True),
+                                       (512, 2048, 8192, False), (200, 136, 96, True)])
+def test_splitk_last_arriver_equals_separate_reduce(monkeypatch, M, N, K, acc):
+    """The fused split-K reduction (the tile's last-arriving slice sums the
+    write-through slabs in slice order, csrc/gemm.hip splitk_tile_reduce)
+    gives the same bits as the separate splitk_reduce_kernel, dW and db,
+    run after run; the ticket words are left zero (a second call on the
+    same workspace is still right)."""
+    O = ops()
+    ldm = (M + 7) // 8 * 8
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    dy = torch.randn(K, ldm, device=dev, generator=g).to(torch.bfloat16)
+    x = torch.randn(K, N, device=dev, generator=g).to(torch.bfloat16)
+    dw0, db0 = torch.randn(M, N, device=dev, generator=g), torch.randn(M, device=dev, generator=g)
+    outs = []
+    for fused in ("0", "1", "1"):
+        monkeypatch.setenv("SMER_SPLITK_FUSED", fused)
+        dw, db = dw0.clone(), db0.clone()
+        O.linear_wgrad(dy, x, dw, M=M, accumulate=acc, db=db)
+        torch.cuda.synchronize()
+        outs.append((dw, db))
+    ref_w = dy[:, :M].float().t() @ x.float() + (dw0 if acc else 0)
+    assert rel_err(outs[1][0], ref_w) < 2e-3
+    for dw, db in outs[1:]:
+        assert torch.equal(dw, outs[0][0]) and torch.equal(db, outs[0][1])
+    ws = O.splitk_workspace(dy.device)
+    assert int(ws[-64 * 1024:].view(torch.int32).abs().sum()) == 0  # tickets reset
+
+
 @pytest.mark.parametrize("M,N,K,acc", [(1536, 768, 16384, True), (3072, 768, 8192, False),
                                        (2304, 768, 32768, True), (4096, 4096, 512, True)])
 def test_gemm256s_wgrad_matches_reference(monkeypatch, M, N, K, acc):

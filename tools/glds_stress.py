@@ -22,7 +22,7 @@ def main():
     T, Mo, Ki = 16384, 768, 768
     dy = torch.randn(T, Mo, device=dev).to(bf)
     x = torch.randn(T, Ki, device=dev).to(bf)
-    ws = torch.empty(ops.SPLITK_WS_BYTES, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(ops.SPLITK_WS_BYTES, dtype=torch.uint8, device=dev)
     # main: attention forward + backward (B 32, H 8, L 1024, D 64) and a dgrad
     B, H, L, D = 32, 8, 1024, 64
     q, k, v = (torch.randn(B * L, H * D, device=dev).to(bf) for _ in range(3))
