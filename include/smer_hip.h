@@ -112,6 +112,15 @@ int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* dy, long ld
                          const void* x, long ldx, float* dW, long lddw, int accumulate,
                          float* db, int db_accumulate, void* workspace, size_t ws_bytes,
                          smer_stream_t stream);
+/* The same with max_workgroups > 0 capping the persistent weight-gradient
+ * grid (0: the whole chip): a weight gradient issued on a second stream
+ * beside the dgrad chain (the overlapped train step) leaves the remaining
+ * CUs to that chain.  The split-K slice count follows the grid, so results
+ * are deterministic for a given cap (not bitwise equal across caps). */
+int smer_gemm_wgrad_bias_ex(int dtype, int M, int N, int K, const void* dy, long lddy,
+                            const void* x, long ldx, float* dW, long lddw, int accumulate,
+                            float* db, int db_accumulate, void* workspace, size_t ws_bytes,
+                            int max_workgroups, smer_stream_t stream);
 
 /* Diagnostics: when buf (device, bytes >= 64 * num_CUs uint64) is non-NULL, the
  * staggered 256x256 GEMM (the forward / dgrad shapes of transformer.py:389-395,

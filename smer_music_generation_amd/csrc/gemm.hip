@@ -48,7 +48,16 @@ struct GemmEpi {
   unsigned* q8_amax;
   // diagnostics (smer_gemm_debug_stamps): per-wave s_memtime phase stamps
   unsigned long long* dbg;
+  // start skew of the persistent 256x256 forward / dgrad kernels (A/B probe,
+  // SMER_G256_SKEW): every second workgroup of an XCD sleeps skew x ~2k
+  // cycles before its first tile, so the all-CU epilogue store bursts of the
+  // two halves no longer coincide
+  int skew;
 };
+__device__ __forceinline__ void g2_start_skew(int skew) {
+  if (skew > 0 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < skew; ++i) __builtin_amdgcn_s_sleep(32);
+}
 
 template <typename T>
 __device__ __forceinline__ void epi_apply(const GemmEpi& e, int M, int N, int row, int col,
@@ -906,6 +915,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_bf16_kernel(int M, int N, int 
   constexpr bool fast = FAST;  // host: gemm256_fast_ok
   const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);
   const long ldx = e.residual ? e.ldr : e.ldg;
+  g2_start_skew(e.skew);
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;
@@ -1236,6 +1246,7 @@ __global__ __launch_bounds__(512, 1) void gemm256s_bf16_kernel(int M, int N, int
 
   unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // e.dbg: tiles 0 and 1, 4 stamps each
   int tcount = 0;
+  g2_start_skew(e.skew);
   for (int jj = braw >> 3; jj < xcount; jj += pstride, ++tcount) {
     const int wgid = xstart + jj;
     const int grp = wgid / (GM * nbn);
@@ -2191,6 +2202,23 @@ static bool smer_gemm256s_enabled(bool bkc, int N, int K) {
   return K >= 1024 || (!bkc && N >= 1024);
 }
 
+// SMER_G256_NONPERSIST (read per call): 1 = the NN dgrad shapes of the
+// 256x256 kernels run one workgroup per tile (grid = tiles) instead of a
+// persistent grid of one per CU, so the hardware dispatcher balances tiles
+// onto the CUs the side-stream weight gradients leave free; 2 = every
+// 256x256 forward / dgrad; 0 = persistent everywhere
+static int smer_g256_nonpersist() {
+  const char* e = getenv("SMER_G256_NONPERSIST");
+  return e ? atoi(e) : 0;
+}
+
+// SMER_G256_SKEW (A/B probe, read per call): start skew of the persistent
+// 256x256 forward / dgrad kernels, in units of ~2k cycles (GemmEpi.skew)
+static int smer_g256_skew() {
+  const char* e = getenv("SMER_G256_SKEW");
+  return e ? std::max(0, std::min(64, atoi(e))) : 0;
+}
+
 // SMER_GEMM64=0 keeps mid-size shapes on the 128x128 kernel (A/B, tests;
 // read per call)
 static bool smer_gemm64_enabled() {
@@ -2254,13 +2282,20 @@ static bool smer_wgrad256s_enabled() {
 // work items of the 256x256 weight-gradient grid (SMER_WGRAD256_SLOTS;
 // default one per CU): fewer split-K slices write fewer fp32 slab bytes and
 // leave CUs to the main stream's kernels (A/B runs)
+// Cap on the persistent weight-gradient grids for the current call
+// (smer_gemm_wgrad_bias_ex max_workgroups; 0 = none): a weight gradient
+// running on a second stream beside the dgrad chain leaves the other CUs to
+// that chain.  Set and cleared around one launch_bf16 call (host thread).
+static thread_local long g_wgrad_cap = 0;
+static long wgrad_cap(long v) { return g_wgrad_cap > 0 ? std::max(8L, std::min(v, g_wgrad_cap)) : v; }
+
 static long smer_wgrad256_slots() {
   static long v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD256_SLOTS");
     v = e ? std::max(8, atoi(e)) : smer_num_cus();
   }
-  return v;
+  return wgrad_cap(v);
 }
 static int smer_wgrad256_depth() {
   static int v = -1;
@@ -2326,7 +2361,7 @@ static long smer_wgrad_resident() {
     const char* e = getenv("SMER_WGRAD_WGP2");
     v = e ? std::max(1, std::min(4, atoi(e))) : 2;
   }
-  return std::max(8L, (v * (long)smer_num_cus()) / 2);
+  return wgrad_cap(std::max(8L, (v * (long)smer_num_cus()) / 2));
 }
 
 // fewest 256x256 tiles for which a forward / dgrad shape takes the 256x256
@@ -2433,15 +2468,20 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
                             hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
         attr_s = true;
       }
-      const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
+      const int np = smer_g256_nonpersist();
+      const bool whole = np == 2 || (np == 1 && !BKC);
+      const int grid = (t2 > smer_num_cus() && !whole) ? (smer_num_cus() & ~7) : (int)t2;
       GemmEpi ed = e;
       ed.dbg = gemm_dbg_for(grid, s);
+      ed.skew = smer_g256_skew();
       hipLaunchKernelGGL(gemm256s_bf16_kernel<BKC>, dim3(grid), dim3(512), G2_LDS, s,
                          M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, ed);
       return;
     }
     if (t2 >= smer_g256_min_tiles()) {
-      const int grid = t2 > smer_num_cus() ? (smer_num_cus() & ~7) : (int)t2;
+      const int np = smer_g256_nonpersist();
+      const bool whole = np == 2 || (np == 1 && !BKC);
+      const int grid = (t2 > smer_num_cus() && !whole) ? (smer_num_cus() & ~7) : (int)t2;
       static bool attr_set = false;  // > 64 KiB dynamic LDS must be opted into
       if (!attr_set) {
         hipFuncSetAttribute((const void*)gemm256_bf16_kernel<AK, BKC, false>,
@@ -2455,8 +2495,10 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       const bool fast = e.vec && e.C && !e.Cf && !e.kv && M % G2 == 0 && N % G2 == 0 &&
                         !(e.residual && e.gate);
       auto kern = fast ? gemm256_bf16_kernel<AK, BKC, true> : gemm256_bf16_kernel<AK, BKC, false>;
+      GemmEpi ek = e;
+      ek.skew = smer_g256_skew();
       hipLaunchKernelGGL(kern, dim3(grid), dim3(512), G2_LDS, s,
-                         M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, e);
+                         M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb, ek);
       return;
     }
   }
@@ -2481,7 +2523,8 @@ static void launch_bf16(int M, int N, int K, const void* A, long lda, const void
       }
       float* rs_part = (split > 1 && rowsum) ? (float*)ws + (size_t)split * M * N : nullptr;
       const long nwg = t2 * split;
-      const int grid = nwg > cus ? (int)(cus & ~7L) : (int)nwg;
+      const long gcap = wgrad_cap(cus);
+      const int grid = nwg > gcap ? (int)(gcap & ~7L) : (int)nwg;
       if (smer_wgrad256s_enabled() && M % G2 == 0 && N % G2 == 0 && e.vec) {
         static bool attr_s = false;
         if (!attr_s) {
@@ -2864,6 +2907,14 @@ extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* 
                                     const void* x, long ldx, float* dW, long lddw, int accumulate,
                                     float* db, int db_accumulate, void* workspace,
                                     size_t ws_bytes, smer_stream_t stream) {
+  return smer_gemm_wgrad_bias_ex(dtype, M, N, K, dy, lddy, x, ldx, dW, lddw, accumulate, db,
+                                 db_accumulate, workspace, ws_bytes, 0, stream);
+}
+
+extern "C" int smer_gemm_wgrad_bias_ex(int dtype, int M, int N, int K, const void* dy, long lddy,
+                                       const void* x, long ldx, float* dW, long lddw, int accumulate,
+                                       float* db, int db_accumulate, void* workspace,
+                                       size_t ws_bytes, int max_workgroups, smer_stream_t stream) {
   SMER_REQUIRE(dtype == SMER_BF16, "smer_gemm_wgrad_bias: bf16 only (fp32: smer_gemm + smer_colsum)");
   SMER_REQUIRE(M > 0 && N > 0 && K > 0, "smer_gemm_wgrad_bias: bad sizes");
   SMER_REQUIRE(dy && x && dW && db, "smer_gemm_wgrad_bias: null pointer");
@@ -2877,7 +2928,9 @@ extern "C" int smer_gemm_wgrad_bias(int dtype, int M, int N, int K, const void* 
   e.Cf = dW; e.ldcf = lddw; e.accumulate = accumulate; e.rs_accumulate = db_accumulate;
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
   e.vec = a16(dW, lddw);
+  g_wgrad_cap = max_workgroups > 0 ? max_workgroups : 0;
   launch_bf16<false, false>(M, N, K, dy, lddy, x, ldx, e, workspace, ws_bytes, (hipStream_t)stream, db);
+  g_wgrad_cap = 0;
   SMER_CHECK_LAUNCH("smer_gemm_wgrad_bias");
   return SMER_OK;
 }
@@ -3551,6 +3604,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   float amax_acc = 0.f;
   const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);  // streamed epilogue operand
   const long ldx = e.residual ? e.ldr : e.ldg;
+  g2_start_skew(e.skew);
 
   for (int jj = braw >> 3; jj < xcount; jj += pstride) {
     const int wgid = xstart + jj;

@@ -48,6 +48,15 @@ class _W:
 FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "0") == "1"
 
 
+# Persistent-grid cap of the weight gradients on the side stream (workgroups;
+# 0 = the whole chip): they then leave the other CUs to the dgrad /
+# attention-backward chain (SMER_WGRAD_SIDE_CAP)
+_WGRAD_SIDE_CAP = int(os.environ.get("SMER_WGRAD_SIDE_CAP", "0"))
+# attention-dropout keep words generated up front on a second stream
+# (SMER_ATTN_MASK_PREGEN=1)
+_ATTN_MASK_PREGEN = os.environ.get("SMER_ATTN_MASK_PREGEN", "0") == "1"
+
+
 class Engine:
     def __init__(self, model):
         self.m = model
@@ -65,6 +74,7 @@ class Engine:
         self._wgen = 0          # bumped whenever the working weights are rewritten
         self._ckv_all = None    # (key, W [L*2d, d], b [L*2d]) stacked cross-attn K/V projections
         self._side = {}         # device -> (wgrad stream, its split-K workspace)
+        self._mstream = {}      # device -> attention-mask generator stream
         self._fp8 = None        # fp8.Fp8Forward (precision "fp8")
 
     # ------------------------------------------------------------------
@@ -316,9 +326,34 @@ class Engine:
         ctx.masks = {}
         keep_mask = save and p_tr > 0 and dt == torch.bfloat16
 
+        # SMER_ATTN_MASK_PREGEN=1: every attention site's keep words are
+        # generated up front on a second stream (VALU-only, beside the
+        # forward's GEMMs) and the forwards read them instead of hashing
+        pregen = {}
+        if keep_mask and _ATTN_MASK_PREGEN:
+            ms = self._mask_stream(dev)
+            ms.wait_stream(torch.cuda.current_stream(dev))
+            sites = [(("enc", i), S, S, sd(_site("enc", i, 0))) for i in range(self.n_enc)]
+            for i in range(self.n_dec):
+                sites += [(("dec", i), T, T, sd(_site("dec", i, 0))), (("cross", i), T, S, sd(_site("dec", i, 2)))]
+            bufs = [ops.attn_drop_mask(B, H, Lq, Lk, dev) for _, Lq, Lk, _ in sites]  # main-stream blocks
+            with torch.cuda.stream(ms):
+                for (key, Lq, Lk, sdv), m_ in zip(sites, bufs):
+                    ops.attn_drop_mask_gen(m_, B=B, H=H, Lq=Lq, Lk=Lk, drop_p=p_tr, seed=sdv)
+                    ev = torch.cuda.Event()
+                    ev.record(ms)
+                    pregen[key] = (m_, ev)
+            for m_ in bufs:
+                m_.record_stream(ms)
+
         def amask(key, Lq, Lk):
             if not keep_mask:
                 return None
+            if key in pregen:
+                m_, ev = pregen[key]
+                torch.cuda.current_stream(dev).wait_event(ev)
+                ctx.masks[key] = m_
+                return m_
             m_ = ops.attn_drop_mask(B, H, Lq, Lk, dev)
             ctx.masks[key] = m_
             return m_
@@ -341,7 +376,7 @@ class Engine:
             q8, oq = self._attn_q8(f8, o, "enc%d.o" % i, D)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=S, Lk=S,
                          D=D, kpm=skpm, causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("enc", i, 0)),
-                         drop_mask=amask(("enc", i), S, S), q8=q8)
+                         drop_mask=amask(("enc", i), S, S), drop_mask_in=bool(pregen), q8=q8)
             y1 = self._lin(f8, o, oq, "enc%d.out" % i, L.out_w, L.out_b, residual=x, drop_p=p_tr,
                            seed=sd(_site("enc", i, 1)))
             x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "enc%d.ln1" % i)
@@ -371,7 +406,7 @@ class Engine:
             q8, oq = self._attn_q8(f8, o, "dec%d.o" % i, D)
             ops.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, lse, B=B, H=H, Lq=T, Lk=T,
                          D=D, kpm=tkpm, causal=True, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 0)),
-                         drop_mask=amask(("dec", i), T, T), q8=q8)
+                         drop_mask=amask(("dec", i), T, T), drop_mask_in=bool(pregen), q8=q8)
             y1 = self._lin(f8, o, oq, "dec%d.sao" % i, L.sa_ow, L.sa_ob, residual=y, drop_p=p_tr,
                            seed=sd(_site("dec", i, 1)))
             x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "dec%d.ln1" % i)
@@ -382,7 +417,7 @@ class Engine:
             q8, ocq = self._attn_q8(f8, oc, "dec%d.oc" % i, D)
             ops.attn_fwd(qc, kvc[:, :d], kvc[:, d:], oc, lsec, B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                          causal=False, scale=scale, drop_p=p_tr, seed=sd(_site("dec", i, 2)),
-                         drop_mask=amask(("cross", i), T, S), q8=q8)
+                         drop_mask=amask(("cross", i), T, S), drop_mask_in=bool(pregen), q8=q8)
             if need_weights:
                 ops.attn_weights(qc, kvc[:, :d], lsec, wts[i], B=B, H=H, Lq=T, Lk=S, D=D, kpm=mkpm,
                                  scale=scale)
@@ -407,6 +442,12 @@ class Engine:
         return logits, wts, ctx
 
     # ------------------------------------------------------------------
+    def _mask_stream(self, dev):
+        ms = self._mstream.get(dev)
+        if ms is None:
+            ms = self._mstream[dev] = torch.cuda.Stream(device=dev)
+        return ms
+
     def _wgrad_stream(self, dev, dt):
         """Weight gradients run on a second HIP stream, overlapping the
         dgrad / attention-backward chain on the main stream (they only feed
@@ -428,7 +469,7 @@ class Engine:
         stream, ws = side
         stream.wait_stream(torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(stream):
-            ops.linear_wgrad(dy, x, gw, ws=ws, **kw)
+            ops.linear_wgrad(dy, x, gw, ws=ws, max_wg=_WGRAD_SIDE_CAP, **kw)
             if ops.CK_LOG is not None:
                 ops.ck("S:dW", gw)
                 ops.ck("S:db", kw.get("db"))

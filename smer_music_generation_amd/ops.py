@@ -202,11 +202,13 @@ def linear_dgrad(dy, w, *, K=None, out=None, residual=None, gate=None, gate_scal
     return out if out is not None else out_f32
 
 
-def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None, ws=None):
+def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None, ws=None, max_wg=0):
     """dw (+)= dy^T @ x: dy [T, M_out(ld)], x [T, K_in] -> dw fp32 [M_out, K_in];
     db (+)= column sums of dy when given (bf16: fused into the GEMM).  `ws`:
     split-K slab buffer (default: the per-device one; a second stream running
-    wgrads concurrently passes its own)."""
+    wgrads concurrently passes its own).  max_wg > 0 caps the persistent
+    weight-gradient grid (smer_gemm_wgrad_bias_ex: leave CUs to a concurrent
+    stream)."""
     T = dy.shape[0]
     Mo = M if M is not None else dy.shape[1]
     if db is not None and dy.dtype == torch.bfloat16:
@@ -217,9 +219,9 @@ def linear_wgrad(dy, x, dw, *, M=None, accumulate=True, db=None, ws=None):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        call("smer_gemm_wgrad_bias", BF16, Mo, x.shape[1], T, _p(dy), _ld(dy), _p(x), _ld(x),
+        call("smer_gemm_wgrad_bias_ex", BF16, Mo, x.shape[1], T, _p(dy), _ld(dy), _p(x), _ld(x),
              _p(dw), _ld(dw), int(accumulate), _p(db), int(accumulate), _p(ws), ws.numel(),
-             _stream())
+             int(max_wg), _stream())
         if timer is not None:
             ev1.record()
             timer.records.append((ev0, ev1, 2.0 * Mo * x.shape[1] * T,
