@@ -18,6 +18,7 @@ Adam semantics (`train.py:264`), as one stream of gfx950 kernels:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -318,6 +319,16 @@ class Trainer:
         grad.zero_()
         hook = None
         bucketer = None
+        self.t += 1
+        work = eng._bf16 if eng.act_dtype() == torch.bfloat16 and eng._bf16 is not None else None
+        g = self.optimizer.param_groups[0]
+        flat = model.flat_parameters()
+
+        def adam(a=None, b=None):
+            sl = slice(a, b)
+            ops.adam(flat[sl], grad[sl], self.m[sl], self.v[sl], work[sl] if work is not None else None,
+                     lr=g["lr"], b1=g["betas"][0], b2=g["betas"][1], eps=g["eps"], step=self.t)
+        stepped = None
         if self.dp:
             if self._bucketer is None or self._bucketer.flat is not grad:
                 # persistent: the bf16 shadow is allocated once
@@ -325,14 +336,30 @@ class Trainer:
                                               wire_dtype=self.grad_wire_dtype)
             bucketer = self._bucketer
             hook = bucketer.reduce
+        elif os.environ.get("SMER_ADAM_OVERLAP", "1") != "0":
+            # Adam of each layer range as soon as its gradients are final: the
+            # hook runs with the weight-gradient stream current, which first
+            # waits for everything the main stream has queued (that layer's
+            # dgrads still read its working weights); elementwise, so the
+            # result is the same bits as one Adam over the flat buffers
+            main = torch.cuda.current_stream(flat.device)
+            stepped = set()
+
+            def hook(name):
+                if name not in self._ranges or name == "embedding":
+                    return
+                torch.cuda.current_stream(flat.device).wait_stream(main)
+                adam(*self._ranges[name])
+                stepped.add(name)
         eng.backward(ctx, dlog, hook=hook)
         if bucketer is not None:
             bucketer.finish()
-        self.t += 1
-        work = eng._bf16 if eng.act_dtype() == torch.bfloat16 and eng._bf16 is not None else None
-        g = self.optimizer.param_groups[0]
-        ops.adam(model.flat_parameters(), grad, self.m, self.v, work, lr=g["lr"], b1=g["betas"][0],
-                 b2=g["betas"][1], eps=g["eps"], step=self.t)
+        if stepped is None:
+            adam()
+        else:  # the ranges no hook stepped (the embedding), on the main stream
+            for name, (a, b) in self._ranges.items():
+                if name not in stepped:
+                    adam(a, b)
         if work is not None:
             eng.mark_bf16_fresh()
         else:
