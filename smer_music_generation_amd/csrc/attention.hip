@@ -1459,9 +1459,14 @@ struct DecQ {
   int dmodel;
 };
 
-template <int D, int NT, int DM>
+// pf(): called once every load of the prologue has been issued (before any
+// of them is used): the caller issues its first K / V key step there, so
+// that step's HBM round trip runs under the prologue's (vmcnt counts in issue
+// order: the prologue's loads are older, so waiting for them leaves the K / V
+// loads in flight)
+template <int D, int NT, int DM, typename PF>
 __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int tid, float* qs,
-                                               bf16* xs, bool need_q, bool store_x) {
+                                               bf16* xs, bool need_q, bool store_x, PF pf) {
   constexpr int TPO = NT / D;    // threads per query value
   constexpr int KT = DM / TPO;   // K per thread (multiple of 8)
   const int lane = tid & 63, wave = tid >> 6;
@@ -1491,6 +1496,9 @@ __device__ __forceinline__ void dec_q_prologue(const DecQ& dq, int h, int r, int
   bf16x8 wv[KT / 8];
 #pragma unroll
   for (int j = 0; j < KT / 8; ++j) wv[j] = *reinterpret_cast<const bf16x8*>(wr + 8 * j);
+  __builtin_amdgcn_sched_barrier(0);
+  pf();
+  __builtin_amdgcn_sched_barrier(0);
   if (wave == 0) {
     float v[NC][8], mu, rs;
 #pragma unroll
@@ -1604,6 +1612,11 @@ __device__ __forceinline__ void dec_q_prologue_f32(const DecQ& dq, int h, int r,
 #ifndef SMER_DEC_QSKIP
 #define SMER_DEC_QSKIP 1  // tools/build_variant.sh ... -DSMER_DEC_QSKIP=0: the A/B baseline
 #endif
+#ifndef SMER_DEC_QLN_EARLY
+// bf16 query prologue: the first K / V key step issued behind the prologue's
+// own loads, before its math (round 6; -DSMER_DEC_QLN_EARLY=0: after it)
+#define SMER_DEC_QLN_EARLY 1
+#endif
 // NS > 0: the keys of a (row, head) split over NS blocks (blockIdx.z), each
 // writing its unnormalised partial {m, l, pad, pad, acc[D]} (fp32, 4 + D
 // floats) to part[((row * H + head) * NS + z) * (4 + D)] instead of o (the
@@ -1663,13 +1676,18 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   // before this step's math (two steps of K / V in flight per lane group;
   // measured 5.2 -> 5.7 TB/s at 4096 keys, slower at 1000)
   uint4 kr[UNR], vr[UNR];
+  constexpr bool early = QP > 0 && sizeof(T) == 2 && SMER_DEC_QLN_EARLY;
   if constexpr (QP > 0) {  // QP = d_model of the query prologue
     __shared__ float qs[LPK * VEC];
     const bool need_q = SMER_DEC_QSKIP ? nk_all > 1 : true;
     const bool store_x = h == 0 && (NS == 0 || blockIdx.z == 0);  // one block per row stores LN(y)
     if constexpr (sizeof(T) == 2) {
       __shared__ __attribute__((aligned(16))) bf16 xs[QP];
-      dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, need_q, store_x);
+      dec_q_prologue<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, need_q, store_x, [&] {
+        if constexpr (early) {
+          if (nk > kb) load_step(kb, kr, vr);
+        }
+      });
     } else {
       __shared__ __attribute__((aligned(16))) float xs[QP];
       dec_q_prologue_f32<LPK * VEC, 64 * NW, QP>(dq, h, r, tid, qs, xs, need_q, store_x);
@@ -1684,7 +1702,7 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
   // memories 46.4k vs 47.5k tokens/s: issued after it.  Without the
   // prologue the first step is requested before q is scaled, in both forms:
   // scaling q first made every block wait for q before its K / V loads.)
-  if ((PIPE || QP == 0) && nk > kb) load_step(kb, kr, vr);
+  if ((PIPE || QP == 0) && !early && nk > kb) load_step(kb, kr, vr);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) qv[i] *= scale;
@@ -1693,7 +1711,7 @@ __global__ __launch_bounds__(64 * NW) void attn_decode_vec_kernel(
     if constexpr (PIPE) {
       if (j0 + KPB * UNR < nk) load_step(j0 + KPB * UNR, kn, vn);
     } else {
-      if (QP != 0 || j0 != kb) load_step(j0, kr, vr);
+      if ((QP != 0 && !early) || j0 != kb) load_step(j0, kr, vr);
     }
     float sc[UNR];
     float mx = m;
