@@ -2325,10 +2325,12 @@ static long smer_skinny16_cap() {  // workgroups per CU (SMER_SKINNY16_CAP; A/B 
   return v;
 }
 
-// Resident split-K workgroups per 2 CUs (SMER_WGRAD_WGP2: 4 = two per CU;
-// 2 = one per CU, the default since round 5: C2 13.49 vs 13.56 ms, C4 fp8
-// 86.84 vs 87.05 ms, three / two interleaved rounds of tools/ab_step.py;
-// 1 = one per two CUs).  The weight gradients run on a second stream beside
+// Resident split-K workgroups per 2 CUs (SMER_WGRAD_WGP2: 4 = two per CU,
+// the default since round 6 -- with the LDS-DMA 128x128 weight gradient back
+// the overlapped C2 step is the same (13.09-13.13 vs 13.08-13.10 ms) and the
+// serialised weight gradients run faster (GEMM family 0.244 vs 0.226 of
+// peak, bench.py's live roofline); 2 = one per CU (round 5: C2 13.49 vs
+// 13.56 ms with register staging); 1 = one per two CUs).  The weight gradients run on a second stream beside
 // the main chain: a smaller persistent grid leaves CUs (and LDS) to the main
 // stream's kernels and cuts the split-K slab bytes in proportion.
 // SMER_WGRAD_STAGES = 2 / 3 / 4: LDS stages of the 128x128 split-K weight
@@ -2359,7 +2361,7 @@ static long smer_wgrad_resident() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SMER_WGRAD_WGP2");
-    v = e ? std::max(1, std::min(4, atoi(e))) : 2;
+    v = e ? std::max(1, std::min(4, atoi(e))) : 4;
   }
   return wgrad_cap(std::max(8L, (v * (long)smer_num_cus()) / 2));
 }
