@@ -129,6 +129,27 @@ __device__ __forceinline__ float max_4groups(float x) {
   const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return vmax_raw(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
+// SMER_ATTN_PRIO (compile time, A/B): raise the issuing wave's priority
+// over its MFMA sections (s_setprio), so that on a SIMD shared by three
+// workgroups' waves the arbiter keeps the matrix pipe fed from whichever
+// wave is in its MFMA section while the others run softmax VALU
+#ifndef SMER_ATTN_PRIO
+#define SMER_ATTN_PRIO 0
+#endif
+__device__ __forceinline__ void attn_prio_hi() {
+  if constexpr (SMER_ATTN_PRIO > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(SMER_ATTN_PRIO);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+__device__ __forceinline__ void attn_prio_lo() {
+  if constexpr (SMER_ATTN_PRIO > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
 }  // namespace
 
 // Attention-dropout keep words, generated once per attention call by
@@ -327,6 +348,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
       if (more) mw_next = mwp[(size_t)(t + 1) * 64];
     }
     f32x4 st[QG][4];
+    attn_prio_hi();
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -338,6 +360,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
         for (int gq = 0; gq < QG; ++gq) st[gq][mt] = mfma16(kf, qf[gq][s], st[gq][mt]);
       }
     }
+    attn_prio_lo();
     if (__builtin_amdgcn_readfirstlane(kpad[cur])) {
       // -inf on padded / out-of-range keys (tiles without any skip this)
 #pragma unroll
@@ -438,6 +461,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
     if constexpr (DROP && !MIN && QG == 2) {
       if (mwo) __builtin_nontemporal_store(kword, mwo + (size_t)t * 64);
     }
+    attn_prio_hi();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -447,6 +471,7 @@ __global__ __launch_bounds__(256, QG == 2 && D > 64 ? 2 : 3) void attn_fwd_bf16(
         for (int gq = 0; gq < QG; ++gq) acc[gq][dt] = mfma16(vf, pf[gq][ks], acc[gq][dt]);
       }
     }
+    attn_prio_lo();
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
@@ -692,6 +717,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
       sf[gk][0] = pack_p(ds, 0);
       sf[gk][1] = pack_p(ds, 1);
     }
+    attn_prio_hi();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -705,6 +731,7 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
         }
       }
     }
+    attn_prio_lo();
     if (more) store(cur ^ 1, t + 1);
     __syncthreads();
   }
@@ -886,6 +913,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
     const char* Ks = sm[cur][0];
     const char* Vs = sm[cur][1];
     f32x4 sacc[QG][4], dpacc[QG][4];
+    attn_prio_hi();
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -904,6 +932,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
         }
       }
     }
+    attn_prio_lo();
     if (__builtin_amdgcn_readfirstlane(kpad[cur])) {
       // -inf on padded / out-of-range keys (tiles without any skip this)
 #pragma unroll
@@ -945,6 +974,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
       sf[gq][0] = pack_p(ds, 0);
       sf[gq][1] = pack_p(ds, 1);
     }
+    attn_prio_hi();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -954,6 +984,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
         for (int gq = 0; gq < QG; ++gq) adq[gq][dt] = mfma16(kt, sf[gq][ks], adq[gq][dt]);
       }
     }
+    attn_prio_lo();
     if (more) {
       tile_store<D>(rk, sm[cur ^ 1][0], tid);
       tile_store<D>(rv, sm[cur ^ 1][1], tid);
