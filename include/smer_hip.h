@@ -387,6 +387,16 @@ int smer_cast2d(int src_dtype, int dst_dtype, int rows, int cols, const void* sr
  * tools/ck_log.py; not on the product path). */
 int smer_debug_checksum(const void* p, long rows, long row_bytes, long ld_bytes,
                         unsigned long long* out, int nparts, smer_stream_t stream);
+/* Validation accuracy counts (train.py:988-1034 `accuracy` inside
+ * validate(), train.py:1037-1195): logits fp32 [R, V] (ld ldl), targets y
+ * int64 [R]; rows with y == pad are skipped; for the others pred = the first
+ * index of the row maximum (torch.argmax) and, with c = cls[y] (int32 [V],
+ * token class ids 0..ncls-1), counts[2c] += 1, counts[2c+1] += (pred == y),
+ * and the same in counts[2 ncls], counts[2 ncls + 1] for the total.
+ * counts: (2 ncls + 2) uint32, accumulated (zero it for one batch). */
+int smer_argmax_accuracy(int R, int V, const float* logits, long ldl, const int64_t* y,
+                         const int32_t* cls, int ncls, int pad, unsigned* counts,
+                         smer_stream_t stream);
 size_t smer_colsum_workspace(int M, int N);
 /* out[n] (+)= sum_m x[m, n] (deterministic two-stage). */
 int smer_colsum(int dtype, int M, int N, const void* x, long ldx, float* out, int accumulate,

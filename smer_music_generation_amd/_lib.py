@@ -118,6 +118,7 @@ SIGNATURES = {
     "smer_colsum_workspace": (c_size, [c_int, c_int]),
     "smer_colsum": (c_int, [c_int, c_int, c_int, P, c_long, P, c_int, P, c_size, P]),
     "smer_debug_checksum": (c_int, [P, c_long, c_long, c_long, P, c_int, P]),
+    "smer_argmax_accuracy": (c_int, [c_int, c_int, P, c_long, P, P, c_int, c_int, P, P]),
 }
 
 _lib = None

@@ -360,3 +360,56 @@ extern "C" int smer_debug_checksum(const void* p, long rows, long row_bytes, lon
   SMER_CHECK_LAUNCH("smer_debug_checksum");
   return SMER_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Validation accuracy (train.py:988-1034 `accuracy`, as validate() calls it):
+// one wave per row; pred = the first index of the row's max logit
+// (torch.argmax), target y; rows whose target is the pad index are skipped;
+// counts[2 c] += 1 and counts[2 c + 1] += (pred == y) for the target's token
+// class c = cls[y], and the same for the total in the last pair (c = ncls).
+// Integer atomics: the counts are exact and order-independent.
+__global__ __launch_bounds__(256) void argmax_acc_kernel(int R, int V, const float* __restrict__ logits,
+                                                         long ldl, const int64_t* __restrict__ y,
+                                                         const int32_t* __restrict__ cls, int ncls,
+                                                         int pad, unsigned* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const long yt = y[r];
+  if (yt == pad) return;
+  const float* x = logits + (long)r * ldl;
+  float best = -INFINITY;
+  int bi = V;  // V: no finite value seen yet (all -inf: index 0, as torch)
+  for (int v = lane; v < V; v += 64) {
+    const float xv = x[v];
+    if (xv > best || bi == V) { best = xv; bi = v; }  // per lane: ascending v, first max kept
+  }
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1) {
+    const float ob = __shfl_xor(best, w, 64);
+    const int oi = __shfl_xor(bi, w, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) {
+    const int c = (yt >= 0 && yt < V) ? cls[yt] : ncls;
+    const unsigned hit = (long)bi == yt ? 1u : 0u;
+    if (c >= 0 && c < ncls) {
+      atomicAdd(counts + 2 * c, 1u);
+      atomicAdd(counts + 2 * c + 1, hit);
+    }
+    atomicAdd(counts + 2 * ncls, 1u);
+    atomicAdd(counts + 2 * ncls + 1, hit);
+  }
+}
+
+extern "C" int smer_argmax_accuracy(int R, int V, const float* logits, long ldl, const int64_t* y,
+                                    const int32_t* cls, int ncls, int pad, unsigned* counts,
+                                    smer_stream_t stream) {
+  SMER_REQUIRE(R >= 0 && V > 0 && ncls >= 0, "smer_argmax_accuracy: bad sizes");
+  SMER_REQUIRE(logits && y && cls && counts, "smer_argmax_accuracy: null pointer");
+  if (R == 0) return SMER_OK;
+  hipLaunchKernelGGL(argmax_acc_kernel, dim3((R + 3) / 4), dim3(256), 0, (hipStream_t)stream, R, V, logits,
+                     ldl, y, cls, ncls, pad, counts);
+  SMER_CHECK_LAUNCH("smer_argmax_accuracy");
+  return SMER_OK;
+}

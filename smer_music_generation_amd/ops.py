@@ -684,6 +684,19 @@ def wce_fwd_bwd(logits, y, w, denom, row_loss, loss_out=None, dlogits=None, *, V
          float(grad_scale), _stream())
 
 
+def argmax_accuracy(logits, y, cls, ncls, pad, counts):
+    """counts[2c], counts[2c+1] += rows / argmax hits of token class c (and
+    the total in the last pair) over the rows whose target is not `pad`
+    (smer_argmax_accuracy; train.py:988-1034)."""
+    R, V = logits.shape
+    if y.dtype != torch.int64 or cls.dtype != torch.int32 or counts.dtype != torch.int32:
+        raise TypeError("argmax_accuracy: int64 targets, int32 class table and counts")
+    if counts.numel() < 2 * ncls + 2:
+        raise ValueError("argmax_accuracy: counts needs 2 * ncls + 2 entries")
+    call("smer_argmax_accuracy", R, V, _p(logits), _ld(logits), _p(y), _p(cls), int(ncls), int(pad),
+         _p(counts), _stream())
+
+
 def adam(p, g, m, v, p_bf16, *, lr, b1, b2, eps, step):
     import math
     bc1 = 1.0 - b1 ** step

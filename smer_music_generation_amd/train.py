@@ -20,6 +20,7 @@ from __future__ import annotations
 import math
 import os
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -368,6 +369,63 @@ class Trainer:
             return loss, self.loss_parts(row_loss, y, denom)
         return loss
 
+    def _class_table(self, dev):
+        """int32 [V] token class id of every vocabulary index (vocab
+        get_token_classes), the class names in id order."""
+        ct = getattr(self, "_cls", None)
+        if ct is None or ct[0].device != dev:
+            v = self.vocab
+            names = sorted(set(v.token_class_ranges.values()))
+            ids = {n: i for i, n in enumerate(names)}
+            # -1: an index with no token class (the reference's `accuracy`
+            # raises KeyError on such a target and validate() skips the batch)
+            tab = torch.tensor([ids.get(v.token_class_ranges.get(i), -1) for i in range(v.vocab_size)],
+                               dtype=torch.int32)
+            ct = self._cls = (tab.to(dev), names)
+        return ct
+
+    def eval_step(self, batch):
+        """The validation pass of one batch (train.py:1037-1195 `validate`
+        body + `accuracy`, train.py:988-1034) on device, no backward: eval
+        forward (no dropout), the fused criteria (no gradient written) and the
+        argmax accuracy counts.  Returns (loss, {criterion: loss}, counts)
+        as device tensors, no host sync; counts int32 [2 * n_classes + 2]
+        (rows, hits per token class in `accuracy_from_counts`' class order,
+        then the total)."""
+        model = self.model
+        eng = model.engine
+        was_training = model.training
+        model.eval()
+        src, tin, tout = batch["input"], batch["target_in"], batch["target_out"]
+        skpm, tkpm = batch["input_pad_mask"], batch["target_pad_mask"]
+        B, T = tin.shape
+        with torch.no_grad():
+            logits, _, _ = eng.forward(src, tin, skpm, tkpm, skpm, training=False,
+                                       need_weights=False, save=False, seed=0)
+            y = tout.reshape(-1).contiguous().long()
+            denom = torch.empty(1, device=logits.device)
+            ops.wce_denom(y, self.ce_all, denom)
+            row_loss = torch.empty(B * T, device=logits.device)
+            loss = torch.empty(1, device=logits.device)
+            ops.wce_fwd_bwd(logits, y, self.w_total, denom, row_loss, loss, None, V=eng.V)
+            parts = self.loss_parts(row_loss, y, denom)
+            cls, names = self._class_table(logits.device)
+            counts = torch.zeros(2 * len(names) + 2, dtype=torch.int32, device=logits.device)
+            ops.argmax_accuracy(logits, y, cls, len(names), self.vocab.pad_index, counts)
+        if was_training:
+            model.train()
+        return loss, parts, counts
+
+    def accuracy_from_counts(self, counts):
+        """{token class: accuracy, 'total': accuracy} as train.py:1022-1026
+        forms it (a class with no target rows keeps 0)."""
+        _, names = self._class_table(self.model.flat_parameters().device)
+        c = counts.detach().to("cpu").numpy().astype(np.int64)
+        out = {}
+        for i, n in enumerate(names + ["total"]):
+            out[n] = float(c[2 * i + 1]) / float(c[2 * i]) if c[2 * i] else 0
+        return out
+
     def loss_parts(self, row_loss, y, denom):
         """Per-criterion losses for logging (train.py:788-797), on device."""
         out = {}
@@ -376,3 +434,28 @@ class Trainer:
                 sel = self.crit_w[name][y] > 0
                 out[name] = (row_loss * sel).sum() / denom[0]
         return out
+
+
+def validate(valid_loader, trainer, device=None):
+    """`validate` (train.py:1037-1195) over a loader of collated batches
+    (dataset.py:856-862 keys) with the fused device pass: per batch the
+    criteria and the accuracy counts stay on device; the dictionaries are
+    averaged over batches as the reference averages them (per-batch loss and
+    per-batch class accuracy, each divided by the number of batches).
+    Returns (total_loss, total_accuracy)."""
+    dev = device or trainer.model.flat_parameters().device
+    total_loss, total_acc, steps = {}, {}, 0
+    for data in iter(valid_loader):
+        bt = {k: (torch.as_tensor(np.asarray(data[k])) if not torch.is_tensor(data[k]) else data[k]).to(dev)
+              for k in ("input", "target_in", "target_out", "input_pad_mask", "target_pad_mask")}
+        loss, parts, counts = trainer.eval_step(bt)
+        steps += 1
+        total_loss["total"] = total_loss.get("total", 0.0) + float(loss.item())
+        for k, v in parts.items():
+            total_loss[k] = total_loss.get(k, 0.0) + float(v.item())
+        for k, v in trainer.accuracy_from_counts(counts).items():
+            total_acc[k] = total_acc.get(k, 0.0) + v
+    for d in (total_loss, total_acc):
+        for k in d:
+            d[k] /= max(steps, 1)
+    return total_loss, total_acc
