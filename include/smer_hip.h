@@ -121,6 +121,19 @@ int smer_gemm_wgrad_bias_ex(int dtype, int M, int N, int K, const void* dy, long
                             const void* x, long ldx, float* dW, long lddw, int accumulate,
                             float* db, int db_accumulate, void* workspace, size_t ws_bytes,
                             int max_workgroups, smer_stream_t stream);
+/* fp8 weight gradient of y = x W^T (transformer.py:389,393,459,463,467 under
+ * train.py:783, precision "fp8"): dW[M,N] (+)= dy_inv * x_inv * dy8^T x8 from
+ * the e4m3 copies dy8 [K, M] (ld lddy bytes) and x8 [K, N] (ld ldx bytes),
+ * K = tokens, with *dy_inv / *x_inv (device) their dequantisation scales.
+ * With db non-NULL also db[M] (+)= dy_inv * sum_t dy8[t, :] (the bias
+ * gradient from the same e4m3 dy).  M, N % 256 == 0, K % 64 == 0 (else
+ * SMER_ERR_UNSUPPORTED, nothing launched); 16-B aligned operands, strides
+ * % 16.  workspace, max_workgroups: as smer_gemm_wgrad_bias_ex (split-K
+ * slabs + M floats per slice, deterministic fixed-order reduce). */
+int smer_gemm_wgrad_fp8(int M, int N, int K, const void* dy8, long lddy, const void* x8, long ldx,
+                        const float* dy_inv, const float* x_inv, float* dW, long lddw, int accumulate,
+                        float* db, int db_accumulate, void* workspace, size_t ws_bytes,
+                        int max_workgroups, smer_stream_t stream);
 
 /* Diagnostics: when buf (device, bytes >= 64 * num_CUs uint64) is non-NULL, the
  * staggered 256x256 GEMM (the forward / dgrad shapes of transformer.py:389-395,

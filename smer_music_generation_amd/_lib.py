@@ -28,6 +28,8 @@ SIGNATURES = {
     "smer_gemm_debug_stamps": (c_int, [P, c_size]),
     "smer_gemm_wgrad_bias": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
                                      c_int, P, c_int, P, c_size, P]),
+    "smer_gemm_wgrad_fp8": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_long, c_int, P, c_int,
+                                    P, c_size, c_int, P]),
     "smer_gemm_wgrad_bias_ex": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
                                         c_int, P, c_int, P, c_size, c_int, P]),
     "smer_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P,

@@ -4223,6 +4223,310 @@ __global__ __launch_bounds__(512, 1) void gemm256s_fp8_kernel(int M, int N, int 
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp8 (e4m3) weight gradient dW (+)= a_inv b_inv dY^T X from tokens-major
+// e4m3 copies of both operands (K = tokens): gemm256s_wgrad_kernel's
+// staggered schedule (four slots, three k-steps ahead, halves one barrier
+// apart, waves 4-7 issue every DMA, waves 0-3 every store) with 64-deep
+// k-steps -- the same 16 KiB per operand per slot, 64 k-rows of 256 B -- on
+// the block-scaled 32x32x64 MFMA (2x the bf16 rate).  The MFMA wants 32
+// consecutive k per lane and the k-rows land tokens-major, so every fragment
+// is four ds_read_b64_tr_b8: in a group of 16 lanes, source lane 2k' + h
+// addresses k-row k' (of 8) at bytes 8h .. 8h+7 of a 16-column block, and
+// lane j receives column j's 8 k-rows (tools/probes/tr8_probe.hip).  The
+// 16-B chunks of k-row k sit at chunk ^ 2 (k & 7): the eight k-rows of one
+// read fall on eight different 32-B bank groups.  Output: alpha * acc into
+// a split-K slab, or dW (+)= alpha * acc unsplit.  The bias gradient rides
+// along from the same e4m3 dY: wave wn sums A fragment wn (32 e4m3 per lane,
+// converted to fp32) on the k-steps j with j % (column tiles) == its column
+// tile, so the extra VALU work is spread evenly over a row of tiles (summed
+// by the first column tile alone it cost the whole grid +20 %: everyone
+// waits for the slowest tile); partials [slice][column tile][M], reduced in
+// fixed order by wgrad_rowsum_reduce_kernel.
+// ---------------------------------------------------------------------------
+namespace {
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ __forceinline__ i32x2 lds_tr8_off(uint32_t a) {
+  i32x2 r;
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+// 32 k of one 32-feature block: k-rows 8r + k' (r = 0..3) of the lane's half
+__device__ __forceinline__ i32x8 tr8_frag(uint32_t a) {
+  const i32x2 r0 = lds_tr8_off<0>(a), r1 = lds_tr8_off<2048>(a);
+  const i32x2 r2 = lds_tr8_off<4096>(a), r3 = lds_tr8_off<6144>(a);
+  return i32x8{r0.x, r0.y, r1.x, r1.y, r2.x, r2.y, r3.x, r3.y};
+}
+// piece t < 4: A k-rows 4c .. 4c+3 (c = 4 lw + t), t >= 4: the B ones
+__device__ __forceinline__ void gw8_piece(int t, uint32_t slot_lds, const uint8_t* At, long lda,
+                                          const uint8_t* Bt, long ldb, int lw, int lane) {
+  const int c = lw * 4 + (t & 3);
+  const int k = c * 4 + (lane >> 4);
+  const int lc = (lane & 15) ^ (2 * (k & 7));
+  if (t < 4)
+    glds16_asm(sgpr_ptr(At), (uint32_t)(k * lda + lc * 16),
+               (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + c * 1024));
+  else
+    glds16_asm(sgpr_ptr(Bt), (uint32_t)(k * ldb + lc * 16),
+               (uint32_t)__builtin_amdgcn_readfirstlane(slot_lds + GS_OP + c * 1024));
+}
+// running fp32 sum of the 32 e4m3 values of a fragment (fixed order)
+__device__ __forceinline__ float rowsum_f8(const i32x8& f, float acc) {
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(f[d], false);
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(f[d], true);
+    p0 += lo[0]; p1 += lo[1]; p0 += hi[0]; p1 += hi[1];
+  }
+  return acc + (p0 + p1);
+}
+__device__ __forceinline__ void gw8_issue(uint32_t slot_lds, const uint8_t* At, long lda, const uint8_t* Bt,
+                                          long ldb, int lw, int lane) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) gw8_piece(t, slot_lds, At, lda, Bt, ldb, lw, lane);
+}
+}  // namespace
+
+__global__ __launch_bounds__(512, 1) void gemm256s_wgrad_fp8_kernel(int M, int N, int K,
+                                                                    const uint8_t* __restrict__ A, long lda,
+                                                                    const uint8_t* __restrict__ B, long ldb,
+                                                                    const float* __restrict__ a_inv,
+                                                                    const float* __restrict__ b_inv,
+                                                                    GemmEpi e, int ksplit, int kchunk,
+                                                                    float* __restrict__ slabs,
+                                                                    float* __restrict__ rowsum) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3, lw = wave & 3;
+  const bool loader = wm == 1;
+  const int nbm = M / G2, nbn = N / G2;
+  const int ntiles = nbm * nbn;
+  const int nwg = ntiles * ksplit;
+  const int braw = blockIdx.x, xcd = braw & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcount = q8 + (xcd < r8 ? 1 : 0);
+  const int pstride = (int)gridDim.x >= nwg ? xcount : ((int)gridDim.x >> 3);
+  constexpr int GM = 4;
+  constexpr int KS = 2 * GS_KS;  // 64 tokens per k-step
+  const float alpha = e.alpha * (*a_inv) * (*b_inv);
+  const float rs_scale = e.alpha * (*a_inv);  // the bias gradient dequantises dY only
+  const uint32_t lds0 = lds_u32(smem);
+  uint32_t aoff[4], boff[2];
+  {
+    const int g = lane >> 4, j = lane & 15, kq = j >> 1, hh = j & 1;
+    const uint32_t krow = (uint32_t)(32 * (g >> 1) + kq) * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] = krow + ((((uint32_t)(8 * wm + 2 * i + (g & 1))) ^ (2 * kq)) << 4) + 8 * hh;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      boff[q] = GS_OP + krow + ((((uint32_t)(4 * wn + 2 * q + (g & 1))) ^ (2 * kq)) << 4) + 8 * hh;
+  }
+
+  for (int jj = braw >> 3; jj < xcount; jj += pstride) {
+    const int lin = xstart + jj;
+    const int split = lin / ntiles, wgid = lin % ntiles;
+    const int grp = wgid / (GM * nbn);
+    const int first_m = grp * GM;
+    const int gsz = min(nbm - first_m, GM);
+    const int within = wgid % (GM * nbn);
+    const int tn = within / gsz;
+    const int m0 = (first_m + within % gsz) * G2, n0 = tn * G2;
+    const int k_begin = split * kchunk, k_end = min(K, k_begin + kchunk);
+    const int nk = (k_end - k_begin) / KS;  // host: >= 1
+    const bool rsum = rowsum != nullptr;
+    const int wn_s = __builtin_amdgcn_readfirstlane(wn);
+    float rs = 0.f;
+
+    f32x16 acc[4][2];  // 32x32 blocks: rows wm*128 + 32 i, columns wn*64 + 32 q
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][q][r] = 0.f;
+    const uint8_t* At = A + (long)k_begin * lda + m0;
+    const uint8_t* Bt = B + (long)k_begin * ldb + n0;
+    const long astep = (long)KS * lda, bstep = (long)KS * ldb;
+
+    if (loader) {
+      gw8_issue(lds0, At, lda, Bt, ldb, lw, lane);
+      if (nk > 1) gw8_issue(lds0 + GS_SLOT, At + astep, lda, Bt + bstep, ldb, lw, lane);
+      if (nk > 2) gw8_issue(lds0 + 2 * GS_SLOT, At + 2 * astep, lda, Bt + 2 * bstep, ldb, lw, lane);
+      if (nk > 2) vm_wait<16>();
+      else if (nk == 2) vm_wait<8>();
+      else vm_wait<0>();
+    }
+    gs_bar();
+    if (loader) gs_bar();
+
+    for (int j = 0; j < nk; ++j) {
+      const uint32_t slot = lds0 + (j & 3) * GS_SLOT;
+      i32x8 af[4], bfr[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) bfr[q] = tr8_frag(slot + boff[q]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = tr8_frag(slot + aoff[i]);
+      const bool do_k = loader && j + 3 < nk;
+      const uint32_t kslot = lds0 + ((j + 3) & 3) * GS_SLOT;
+      const uint8_t* Aj = At + (long)(j + 3) * astep;
+      const uint8_t* Bj = Bt + (long)(j + 3) * bstep;
+      if (do_k) {
+#pragma unroll
+        for (int t = 4; t < 8; ++t) gw8_piece(t, kslot, Aj, lda, Bj, ldb, lw, lane);
+      }
+      if (loader) {
+        if (j + 3 < nk) vm_wait<12>();
+        else if (j + 3 == nk) vm_wait<8>();
+        else if (j + 2 == nk) vm_wait<0>();
+      }
+      gs_bar();
+      f8_retire(af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) acc[i][q] = mfma_f8_32(af[i], bfr[q], acc[i][q]);
+        if (do_k) {  // one A piece of k-step j+3 behind every 2 MFMAs (64 cycles each)
+          __builtin_amdgcn_sched_barrier(0);
+          gw8_piece(i, kslot, Aj, lda, Bj, ldb, lw, lane);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      if (rsum && j % nbn == tn) {  // wave wn: A fragment wn (rows wm*128 + 32 wn + (lane & 31))
+        if (wn_s == 0) rs = rowsum_f8(af[0], rs);
+        else if (wn_s == 1) rs = rowsum_f8(af[1], rs);
+        else if (wn_s == 2) rs = rowsum_f8(af[2], rs);
+        else rs = rowsum_f8(af[3], rs);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      gs_bar();
+    }
+    if (!loader) gs_bar();  // realign the halves (every wave past its last reads)
+    if (rsum) {
+      rs += __shfl_xor(rs, 32);  // the two k-halves of a row
+      if (lane < 32) {
+        const int row = m0 + wm * 128 + 32 * wn + lane;
+        rowsum[((long)split * nbn + tn) * M + row] = rs * rs_scale;
+      }
+    }
+
+    // ---- epilogue: eight 32-row passes through fp32 staging (slot 2)
+    float* ep = reinterpret_cast<float*>(smem + GS_EP);
+    float* slab = ksplit > 1 ? slabs + (long)split * M * N : nullptr;
+    const int ch = tid & 31;
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      if (wm == (pass >> 2)) {  // 32x32 row block i = pass & 3: row (r&3) + 8 (r>>2) + 4 (lane>>5)
+        const int i = pass & 3;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            ep[gs_ep_idx32((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), wn * 64 + q * 32 + (lane & 31))] =
+                acc[i][q][r];
+      }
+      smer_lds_barrier();
+      if (!loader) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int row = (tid >> 5) + 8 * c;  // 0..31
+          const long grow = m0 + pass * GS_EPR + row;
+          const int gcol = n0 + ch * 8;
+          float4 a = *reinterpret_cast<const float4*>(ep + gs_ep_idx32(row, ch * 8));
+          float4 b = *reinterpret_cast<const float4*>(ep + gs_ep_idx32(row, ch * 8) + 4);
+          a.x *= alpha; a.y *= alpha; a.z *= alpha; a.w *= alpha;
+          b.x *= alpha; b.y *= alpha; b.z *= alpha; b.w *= alpha;
+          float* dst = slab ? slab + grow * N + gcol : e.Cf + grow * e.ldcf + gcol;
+          if (!slab && e.accumulate) {
+            const float4 o0 = *reinterpret_cast<const float4*>(dst);
+            const float4 o1 = *reinterpret_cast<const float4*>(dst + 4);
+            a.x += o0.x; a.y += o0.y; a.z += o0.z; a.w += o0.w;
+            b.x += o1.x; b.y += o1.y; b.z += o1.z; b.w += o1.w;
+          }
+          *reinterpret_cast<float4*>(dst) = a;
+          *reinterpret_cast<float4*>(dst + 4) = b;
+        }
+      }
+      smer_lds_barrier();
+    }
+  }
+}
+
+// db[m] (+)= sum_p part[p][m], p in order (deterministic)
+__global__ void wgrad_rowsum_reduce_kernel(int M, int nparts, const float* __restrict__ part,
+                                           float* __restrict__ db, int accumulate) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float t = 0.f;
+  for (int p = 0; p < nparts; ++p) t += part[(long)p * M + m];
+  db[m] = (accumulate ? db[m] : 0.f) + t;
+}
+
+// dW[M, N] (+)= dy_inv x_inv sum_t dy8[t, m] x8[t, n],
+// db[M] (+)= dy_inv sum_t dy8[t, m]  (K = tokens)
+extern "C" int smer_gemm_wgrad_fp8(int M, int N, int K, const void* dy8, long lddy, const void* x8, long ldx,
+                                   const float* dy_inv, const float* x_inv, float* dW, long lddw, int accumulate,
+                                   float* db, int db_accumulate, void* workspace, size_t ws_bytes,
+                                   int max_workgroups, smer_stream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % G2 || N % G2 || K % (2 * GS_KS))
+    return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm_wgrad_fp8: needs M, N % 256 == 0 and K % 64 == 0");
+  SMER_REQUIRE(dy8 && x8 && dy_inv && x_inv && dW && (!db || workspace), "smer_gemm_wgrad_fp8: null pointer");
+  SMER_REQUIRE(aligned16(dy8) && aligned16(x8) && lddy % 16 == 0 && ldx % 16 == 0 && lddy >= M && ldx >= N &&
+                   aligned16(dW) && lddw % 4 == 0 && lddw >= N && (!workspace || aligned16(workspace)),
+               "smer_gemm_wgrad_fp8: operand strides / alignment");
+  hipStream_t s = (hipStream_t)stream;
+  GemmEpi e{};
+  e.alpha = 1.f; e.drop_scale = 1.f;
+  e.Cf = dW; e.ldcf = lddw; e.accumulate = accumulate; e.vec = 1; e.rs_accumulate = db_accumulate;
+  g_wgrad_cap = max_workgroups > 0 ? max_workgroups : 0;
+  const long t2 = (long)(M / G2) * (N / G2);
+  const int nbn = N / G2;
+  const long cus = smer_num_cus();
+  long ns = std::min<long>(smer_wgrad256_slots() / t2, K / smer_wgrad256_depth());
+  // per slice: an M x N slab and nbn x M bias partials
+  ns = std::min<long>(ns, (long)(splitk_slab_bytes(workspace ? ws_bytes : 0) /
+                                 (((size_t)M * N + (size_t)nbn * M) * sizeof(float))));
+  ns = std::max<long>(1, std::min<long>(ns, 64));
+  const int KS = 2 * GS_KS;
+  const int kchunk = (int)(((K + ns - 1) / ns + KS - 1) / KS * KS);
+  const int split = (K + kchunk - 1) / kchunk;
+  const long nwg = t2 * split;
+  const long gcap = wgrad_cap(cus);
+  g_wgrad_cap = 0;
+  const int grid = nwg > gcap ? (int)(gcap & ~7L) : (int)nwg;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm256s_wgrad_fp8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        4 * GS_SLOT);
+    attr = true;
+  }
+  // split-K: alpha-scaled slabs, then the bias partials
+  const size_t slab_floats = split > 1 ? (size_t)split * M * N : 0;
+  float* rs_part = db ? (float*)workspace + slab_floats : nullptr;
+  if (db && (slab_floats + (size_t)split * nbn * M) * sizeof(float) > splitk_slab_bytes(ws_bytes))
+    return smer_set_error(SMER_ERR_INVALID, "smer_gemm_wgrad_fp8: workspace too small for the bias partials");
+  hipLaunchKernelGGL(gemm256s_wgrad_fp8_kernel, dim3(grid), dim3(512), 4 * GS_SLOT, s, M, N, K,
+                     (const uint8_t*)dy8, lddy, (const uint8_t*)x8, ldx, dy_inv, x_inv, e, split, kchunk,
+                     (float*)workspace, rs_part);
+  if (split > 1) {
+    const long n4 = ((long)M * N) / 4;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((n4 + 255) / 256), dim3(256), 0, s, M, N, split,
+                       (const float*)workspace, 1.f, dW, lddw, accumulate, (const float*)nullptr, (float*)nullptr,
+                       0);
+  }
+  if (db)
+    hipLaunchKernelGGL(wgrad_rowsum_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, split * nbn,
+                       (const float*)rs_part, db, db_accumulate);
+  SMER_CHECK_LAUNCH("smer_gemm_wgrad_fp8");
+  return SMER_OK;
+}
+
 
 extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                                const float* a_inv, const float* b_inv, const float* bias, int relu,

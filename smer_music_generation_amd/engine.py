@@ -322,6 +322,9 @@ class Engine:
         ctx.B, ctx.S, ctx.T, ctx.dt, ctx.p_pos, ctx.p_tr, ctx.seed = B, S, T, dt, p_pos, p_tr, seed
         ctx.src_ids, ctx.tgt_ids, ctx.skpm, ctx.tkpm, ctx.mkpm = src_ids, tgt_ids, skpm, tkpm, mkpm
         ctx.enc, ctx.dec = [], []
+        # fp8: the e4m3 copies of each layer's weight-gradient inputs X (None
+        # where a site has no copy / no scale history yet)
+        ctx.enc_q, ctx.dec_q = [], []
         # attention-dropout keep bits written by the forward, read by backward
         ctx.masks = {}
         keep_mask = save and p_tr > 0 and dt == torch.bfloat16
@@ -370,6 +373,7 @@ class Engine:
         ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
         xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)
         for i, L in enumerate(W.enc):
+            xq_in = xq
             qkv = self._lin(f8, x, xq, "enc%d.in" % i, L.in_w, L.in_b)
             o = torch.empty(B * S, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, S, device=dev)
@@ -388,10 +392,12 @@ class Engine:
                                         "enc%d.ln2" % i if i + 1 < self.n_enc else None)
             if save:
                 ctx.enc.append((x, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2))
+                ctx.enc_q.append((xq_in, oq, x1q, hq))
             x = x2
         mem, me, re, memq = self._ln_q(f8, x, W.enc_norm, dt, "mem")
         ctx.enc_last = (x, me, re)
         ctx.mem = mem
+        ctx.memq = memq
 
         y = torch.empty(B * T, d, dtype=dt, device=dev)
         ops.embed(tgt_ids, W.emb, pe2, y, L=T, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_tgt"]))
@@ -400,6 +406,7 @@ class Engine:
         kvc_all = self._lin(f8, mem, memq, "ckv", W.ckv_all, W.ckv_b_all) if self.n_dec else None
         yq = None
         for i, L in enumerate(W.dec):
+            yq_in = yq
             qkv = self._lin(f8, y, yq, "dec%d.sa" % i, L.sa_w, L.sa_b)
             o = torch.empty(B * T, d, dtype=dt, device=dev)
             lse = torch.empty(B, H, T, device=dev)
@@ -433,6 +440,7 @@ class Engine:
             if save:
                 ctx.dec.append((y, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2,
                                 h, y3, m3, r3))
+                ctx.dec_q.append((yq_in, oq, x1q, ocq, x2q, hq))
             y = x3
         out, mo, ro = self._ln(y, W.dec_norm, dt)
         ctx.dec_last = (y, mo, ro)
@@ -462,14 +470,23 @@ class Engine:
         return side
 
     @staticmethod
-    def _wgrad(side, dy, x, gw, **kw):
+    def _wgrad(side, dy, x, gw, q8=None, **kw):
+        """dW (+ db) of one Linear, on the side stream when there is one.
+        q8 = (dy e4m3, its inv scale, x e4m3, its inv scale): the fp8 weight
+        gradient (smer_gemm_wgrad_fp8), bf16 when its shape does not tile."""
+        def run(ws, cap):
+            if q8 is not None and ops.linear_wgrad_fp8(q8[0], q8[1], q8[2], q8[3], gw, db=kw.get("db"),
+                                                       accumulate=kw.get("accumulate", True), ws=ws,
+                                                       max_wg=cap):
+                return
+            ops.linear_wgrad(dy, x, gw, ws=ws, max_wg=cap, **kw)
         if side is None:
-            ops.linear_wgrad(dy, x, gw, **kw)
+            run(None, 0)
             return
         stream, ws = side
         stream.wait_stream(torch.cuda.current_stream(dy.device))
         with torch.cuda.stream(stream):
-            ops.linear_wgrad(dy, x, gw, ws=ws, max_wg=_WGRAD_SIDE_CAP, **kw)
+            run(ws, _WGRAD_SIDE_CAP)
             if ops.CK_LOG is not None:
                 ops.ck("S:dW", gw)
                 ops.ck("S:db", kw.get("db"))
@@ -479,6 +496,9 @@ class Engine:
         # side stream has read them
         dy.record_stream(stream)
         x.record_stream(stream)
+        if q8 is not None:
+            q8[0].record_stream(stream)
+            q8[2].record_stream(stream)
 
     @staticmethod
     def _join(side):
@@ -578,7 +598,16 @@ class Engine:
         # vocab head
         side = self._wgrad_stream(dev, dt)
         ps = side[0] if side is not None else None  # LayerNorm dgamma / dbeta reductions too
-        wg = lambda *a, **kw: self._wgrad(side, *a, **kw)  # noqa: E731
+        wg_ = lambda *a, **kw: self._wgrad(side, *a, **kw)  # noqa: E731
+        from .fp8 import FP8_WGRAD
+        f8w = ctx.f8 if FP8_WGRAD else None
+
+        def wg(dy_, x_, gw, dyq=None, xq=None, **kw):
+            """weight gradient; on the fp8 MFMA when both operands have a
+            usable e4m3 copy ((tensor, site) pairs)"""
+            if f8w is not None and dyq is not None and xq is not None:
+                kw["q8"] = (dyq[0], f8w.inv_of(dyq[1]), xq[0], f8w.inv_of(xq[1]))
+            wg_(dy_, x_, gw, **kw)
         ops.ck("M:dlog", dlog_pad)
         wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
@@ -604,16 +633,17 @@ class Engine:
             L, GL = W.dec[i], G.dec[i]
             (y_in, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2, h, y3, m3,
              r3) = ctx.dec[i]
+            yq_in, oq, x1q, ocq, x2q, hq = ctx.dec_q[i]
             # FFN block: x3 = LN3(x2 + drop(W2 drop(relu(W1 x2))))
             dy3 = torch.empty_like(y3)
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
             ck("M:dec%d.dy3" % i, dy3d)
-            wg(dy3d, h, GL.l2_w, db=GL.l2_b)
+            wg(dy3d, h, GL.l2_w, dy3q, hq, db=GL.l2_b)
             dh, dhq = dgrad(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, q_site="b.dec%d.dh" % i, gate=h,
                             gate_scale=ops.drop_scale(p_tr))
             ck("M:dec%d.dh" % i, dh)
-            wg(dh, x2, GL.l1_w, db=GL.l1_b)
+            wg(dh, x2, GL.l1_w, dhq, x2q, db=GL.l1_b)
             dx2, _ = dgrad(dhq, dh, "dec%d.l1" % i, L.l1_w, residual=dy3)
             ck("M:dec%d.dx2" % i, dx2)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
@@ -621,7 +651,7 @@ class Engine:
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx2, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("dec", i, 3)), GL.n2, "b.dec%d.ln2" % i)
             ck("M:dec%d.dy2" % i, dy2d)
-            wg(dy2d, oc, GL.ca_ow, db=GL.ca_ob)
+            wg(dy2d, oc, GL.ca_ow, dy2q, ocq, db=GL.ca_ob)
             doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
             ck("M:dec%d.doc" % i, doc)
             dqc = torch.empty(Mt, d, dtype=dt, device=dev)
@@ -640,8 +670,11 @@ class Engine:
                          q8=q8c)
             ck("M:dec%d.dqc" % i, dqc)
             ck("M:dec%d.dkvc" % i, dkvc)
-            wg(dqc, x1, GL.cq_w, db=GL.cq_b)
-            wg(dkvc, ctx.mem, GL.ckv_w, db=GL.ckv_b)
+            wg(dqc, x1, GL.cq_w, dqcq, x1q, db=GL.cq_b)
+            dkvcq = None
+            if cross8 is not None and "b.cross" in f8.bwd_ready:
+                dkvcq = (cross8[1][:, i * 2 * d:(i + 1) * 2 * d], cross8[0])
+            wg(dkvc, ctx.mem, GL.ckv_w, dkvcq, ctx.memq, db=GL.ckv_b)
             dx1, _ = dgrad(dqcq, dqc, "dec%d.cq" % i, L.cq_w, residual=dy2)
             ck("M:dec%d.dx1" % i, dx1)
             # self-attention block
@@ -649,7 +682,7 @@ class Engine:
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("dec", i, 1)), GL.n1, "b.dec%d.ln1" % i)
             ck("M:dec%d.dy1" % i, dy1d)
-            wg(dy1d, o, GL.sa_ow, db=GL.sa_ob)
+            wg(dy1d, o, GL.sa_ow, dy1q, oq, db=GL.sa_ob)
             do, _ = dgrad(dy1q, dy1d, "dec%d.sao" % i, L.sa_ow)
             ck("M:dec%d.do" % i, do)
             dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
@@ -659,7 +692,7 @@ class Engine:
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
                          seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)), q8=q8s)
             ck("M:dec%d.dqkv" % i, dqkv)
-            wg(dqkv, y_in, GL.sa_w, db=GL.sa_b)
+            wg(dqkv, y_in, GL.sa_w, dqkvq, yq_in, db=GL.sa_b)
             dy, _ = dgrad(dqkvq, dqkv, "dec%d.sa" % i, L.sa_w, residual=dy1)
             ck("M:dec%d.dy" % i, dy)
             if hook:
@@ -684,22 +717,23 @@ class Engine:
         for i in reversed(range(self.n_enc)):
             L, GL = W.enc[i], G.enc[i]
             (x_in, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2) = ctx.enc[i]
+            xq_in, oq, x1q, hq = ctx.enc_q[i]
             dy2 = torch.empty_like(y2)
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
             ck("M:enc%d.dy2" % i, dy2d)
-            wg(dy2d, h, GL.l2_w, db=GL.l2_b)
+            wg(dy2d, h, GL.l2_w, dy2q, hq, db=GL.l2_b)
             dh, dhq = dgrad(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, q_site="b.enc%d.dh" % i, gate=h,
                             gate_scale=ops.drop_scale(p_tr))
             ck("M:enc%d.dh" % i, dh)
-            wg(dh, x1, GL.l1_w, db=GL.l1_b)
+            wg(dh, x1, GL.l1_w, dhq, x1q, db=GL.l1_b)
             dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)
             ck("M:enc%d.dx1" % i, dx1)
             dy1 = torch.empty_like(y1)
             dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("enc", i, 1)), GL.n1, "b.enc%d.ln1" % i)
             ck("M:enc%d.dy1" % i, dy1d)
-            wg(dy1d, o, GL.out_w, db=GL.out_b)
+            wg(dy1d, o, GL.out_w, dy1q, oq, db=GL.out_b)
             do, _ = dgrad(dy1q, dy1d, "enc%d.out" % i, L.out_w)
             ck("M:enc%d.do" % i, do)
             dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
@@ -709,7 +743,7 @@ class Engine:
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
                          seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)), q8=q8s)
             ck("M:enc%d.dqkv" % i, dqkv)
-            wg(dqkv, x_in, GL.in_w, db=GL.in_b)
+            wg(dqkv, x_in, GL.in_w, dqkvq, xq_in, db=GL.in_b)
             dx, _ = dgrad(dqkvq, dqkv, "enc%d.in" % i, L.in_w, residual=dy1)
             ck("M:enc%d.dx" % i, dx)
             if hook:

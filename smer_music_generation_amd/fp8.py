@@ -23,7 +23,11 @@ switches to fp8 once it has one step of history (the first step's backward
 is bf16).  W^T copies are quantised with the forward copies, once per
 optimizer step.  The memory dgrad (K = 12 * 2d) reads one e4m3 copy of
 every layer's cross-attention dK | dV under a single scale site (shared with
-the cross dQ copies).  Every weight gradient stays bf16.
+the cross dQ copies).  Weight gradients (FP8_WGRAD, round 6): dW =
+e4m3(dY)^T e4m3(X) wherever both copies exist (every one but FFN2's, whose X
+copy needs engine.FP8_FFN2, and the first layers' QKV), through the
+transposing 8-bit LDS reads of smer_gemm_wgrad_fp8; the bias gradient from
+the same e4m3 dY.
 
 Scaling (no standalone quantise pass over activations):
   * every producer (LayerNorm, the FFN1 epilogue) writes an e4m3 copy
@@ -55,6 +59,11 @@ FP8_ATTN_DGRAD = os.environ.get("SMER_FP8_ATTN_DGRAD", "1") != "0"
 # fp8 attention out-projections in the forward: the attention kernel writes
 # the e4m3 copy of its output (SMER_FP8_ATTN_OUT=0: bf16, A/B)
 FP8_ATTN_OUT = os.environ.get("SMER_FP8_ATTN_OUT", "1") != "0"
+# fp8 weight gradients dW = e4m3(dY)^T e4m3(X) (and db from the same e4m3
+# dY) wherever both copies exist: the backward's dY copies above and the
+# forward's X copies (LayerNorm outputs, attention outputs, FFN1's output
+# with engine.FP8_FFN2) (SMER_FP8_WGRAD=0: bf16 weight gradients, A/B)
+FP8_WGRAD = os.environ.get("SMER_FP8_WGRAD", "1") != "0"
 
 # forward contraction groups that run on the fp8 MFMA (tests / tools switch
 # groups off to measure each one's numerical effect): "qkv" self-attention

@@ -479,6 +479,30 @@ def gemm_fp8_ex(a8, a_inv, b8, b_inv, out, *, bias=None, residual=None, gate=Non
     return True
 
 
+def linear_wgrad_fp8(dy8, dy_inv, x8, x_inv, dw, *, accumulate=True, db=None, ws=None, max_wg=0):
+    """dw fp32 [M, N] (+)= dy_inv*x_inv * dy8^T @ x8 from the tokens-major
+    e4m3 copies dy8 [T, M] and x8 [T, N] (precision "fp8" weight gradients),
+    db (+)= dy_inv * column sums of dy8 when given.  Returns False (nothing
+    launched) outside the kernel's tiling (M, N % 256, T % 64)."""
+    T, M = dy8.shape
+    N = x8.shape[1]
+    if M % 256 or N % 256 or T % 64 or x8.shape[0] != T or tuple(dw.shape) != (M, N):
+        return False
+    if ws is None:
+        ws = splitk_workspace(dy8.device)
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    call("smer_gemm_wgrad_fp8", M, N, T, _p(dy8), _ld(dy8), _p(x8), _ld(x8), _p(dy_inv), _p(x_inv), _p(dw),
+         _ld(dw), int(accumulate), _p(db), int(accumulate), _p(ws), ws.numel(), int(max_wg), _stream())
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * T, "fp8 wgrad M%d N%d K%d" % (M, N, T)))
+    return True
+
+
 def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
              seed=0):
     """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ epilogue).  Returns False

@@ -1356,3 +1356,52 @@ def test_layernorm_bwd_t4_kernel(M, N, monkeypatch):
     torch.nn.functional.layer_norm(xf, (N,), gf, bf, 1e-5).backward(dy.float())
     assert rel_err(new[0], xf.grad) < 2e-2
     assert rel_err(new[2], gf.grad) < 1e-2 and rel_err(new[3], bf.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,T,acc,strided", [(256, 256, 64, False, False), (256, 512, 192, True, False),
+                                               (768, 512, 4096, True, True), (2304, 768, 16384, False, False),
+                                               (768, 3072, 8192, True, False)])
+def test_wgrad_fp8_exact_integer_layout(M, N, T, acc, strided):
+    """fp8 weight gradient (tokens-major e4m3 operands through the transposing
+    8-bit LDS reads, split-K slabs, fused bias gradient) on exact small-
+    integer data and power-of-two scales: every partial sum is exact in fp32,
+    so dW must equal s_dy * s_x * dY^T X and db s_dy * colsum(dY) bit for bit
+    (plus the old values when accumulating).
+    Covers one k-step (T = 64), the 3-step prologue edge, split-K, an
+    operand that is a column slice of a wider buffer, and the C4 shapes."""
+    O = ops()
+    g = torch.Generator(device="cpu").manual_seed(M + N + T)
+    dY = torch.randint(-4, 5, (T, M), generator=g).float()
+    X = torch.randint(-3, 4, (T, N), generator=g).float()
+    X[:, 0] += torch.arange(T) % 5  # asymmetric
+    dy8 = dY.to(torch.float8_e4m3fn).view(torch.uint8)
+    if strided:  # the column slice of a wider e4m3 buffer (dQKV's copy)
+        wide = torch.zeros(T, M + 256, dtype=torch.uint8)
+        wide[:, 128:128 + M] = dy8
+        dy8 = wide.to(dev)[:, 128:128 + M]
+    else:
+        dy8 = dy8.to(dev)
+    x8 = X.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    si, xi = torch.tensor([0.5], device=dev), torch.tensor([0.25], device=dev)
+    old = torch.randint(-8, 9, (M, N), generator=g).float()
+    dw = old.to(dev) if acc else torch.full((M, N), float("nan"), device=dev)
+    oldb = torch.randint(-8, 9, (M,), generator=g).float()
+    db = oldb.to(dev) if acc else torch.full((M,), float("nan"), device=dev)
+    assert O.linear_wgrad_fp8(dy8, si, x8, xi, dw, accumulate=acc, db=db)
+    ref = (dY.t() @ X) * 0.125 + (old if acc else 0.0)
+    refb = dY.sum(0) * 0.5 + (oldb if acc else 0.0)
+    torch.cuda.synchronize()
+    assert torch.equal(dw.cpu(), ref)
+    assert torch.equal(db.cpu(), refb)
+    dw2 = torch.zeros(M, N, device=dev)  # without the bias gradient: the same dW
+    assert O.linear_wgrad_fp8(dy8, si, x8, xi, dw2, accumulate=False)
+    torch.cuda.synchronize()
+    assert torch.equal(dw2.cpu(), (dY.t() @ X) * 0.125)
+
+
+def test_wgrad_fp8_declines_outside_tiling():
+    O = ops()
+    z = torch.zeros(64, 200, dtype=torch.uint8, device=dev)
+    one = torch.ones(1, device=dev)
+    dw = torch.zeros(200, 200, device=dev)
+    assert not O.linear_wgrad_fp8(z, one, z, one, dw)
