@@ -4458,13 +4458,24 @@ __global__ __launch_bounds__(512, 1) void gemm256s_wgrad_fp8_kernel(int M, int N
   }
 }
 
-// db[m] (+)= sum_p part[p][m], p in order (deterministic)
-__global__ void wgrad_rowsum_reduce_kernel(int M, int nparts, const float* __restrict__ part,
-                                           float* __restrict__ db, int accumulate) {
+// db[m] (+)= sum_p part[p][m], p in order (deterministic).  64-thread
+// blocks (M / 64 of them) with 8 partial loads in flight per thread: a
+// serial chain of dependent-latency loads ran ~50 us per call beside the
+// main stream's kernels.
+__global__ __launch_bounds__(64) void wgrad_rowsum_reduce_kernel(int M, int nparts, const float* __restrict__ part,
+                                                                 float* __restrict__ db, int accumulate) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
   float t = 0.f;
-  for (int p = 0; p < nparts; ++p) t += part[(long)p * M + m];
+  int p = 0;
+  for (; p + 8 <= nparts; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(long)(p + u) * M + m];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; p < nparts; ++p) t += part[(long)p * M + m];
   db[m] = (accumulate ? db[m] : 0.f) + t;
 }
 
@@ -4521,7 +4532,7 @@ extern "C" int smer_gemm_wgrad_fp8(int M, int N, int K, const void* dy8, long ld
                        0);
   }
   if (db)
-    hipLaunchKernelGGL(wgrad_rowsum_reduce_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, split * nbn,
+    hipLaunchKernelGGL(wgrad_rowsum_reduce_kernel, dim3((M + 63) / 64), dim3(64), 0, s, M, split * nbn,
                        (const float*)rs_part, db, db_accumulate);
   SMER_CHECK_LAUNCH("smer_gemm_wgrad_fp8");
   return SMER_OK;

@@ -8,7 +8,7 @@ from collections import defaultdict
 
 path = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-marker = re.compile(sys.argv[3] if len(sys.argv) > 3 else r"^wce_denom_kernel")  # once per step (Adam runs per layer range since round 6)
+marker = re.compile(sys.argv[3] if len(sys.argv) > 3 else r"^embed_bwd_reduce")  # once per step, at the end of backward
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if marker.search(r["Kernel_Name"])]
