@@ -730,8 +730,11 @@ def main():
                                 "dtype": "fp8 (e4m3 forward GEMMs: QKV, attention out-"
                                          "projections, FFN1, cross-attention Q and K/V; e4m3 "
                                          "dgrads: FFN2, FFN1, out-projections, QKV, cross Q, "
-                                         "memory; delayed per-tensor scaling; weight gradients, "
-                                         "attention, FFN2 forward and the vocab head bf16)",
+                                         "memory; e4m3 weight + bias gradients: QKV (layers >= 1), "
+                                         "out-projections, FFN1, cross Q and K/V; delayed "
+                                         "per-tensor scaling; attention, FFN2 forward and weight "
+                                         "gradient, first-layer QKV weight gradients and the "
+                                         "vocab head bf16)",
                                 "value": round(c4["tokens_per_s"], 1),
                                 "ms_per_step": round(c4["ms_per_step"], 2),
                                 "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),
