@@ -1,7 +1,8 @@
 """Median time (us) of every C2 forward / dgrad GEMM shape under the
 current environment (dispatch switches read once per process), beside
 hipBLASLt: run it in one process per configuration to A/B static switches.
-    SMER_G256_MIN=300 python tools/shape_times.py"""
+    SMER_G256_MIN=300 python tools/shape_times.py [dec]
+"dec": the decoder's shapes (M = B*T = 8192 rows) instead of the encoder's."""
 import os
 import sys
 
@@ -16,7 +17,15 @@ bf = torch.bfloat16
 
 def main():
     tag = " ".join("%s=%s" % (k, v) for k, v in sorted(os.environ.items()) if k.startswith("SMER_"))
-    for name, M, N, K, bk, epi in SHAPES[:9]:
+    shapes = SHAPES[:9]
+    if len(sys.argv) > 1 and sys.argv[1] == "dec":
+        shapes = [("dec fwd qkv", 8192, 1536, 512, True, "b"), ("dec fwd out", 8192, 512, 512, True, "bRd"),
+                  ("dec fwd cq", 8192, 512, 512, True, "b"), ("dec fwd ffn1", 8192, 2048, 512, True, "brd"),
+                  ("dec fwd ffn2", 8192, 512, 2048, True, "bRd"),
+                  ("dec dgrad ffn2", 8192, 2048, 512, False, "g"), ("dec dgrad ffn1", 8192, 512, 2048, False, "R"),
+                  ("dec dgrad out", 8192, 512, 512, False, ""), ("dec dgrad qkv", 8192, 512, 1536, False, "R"),
+                  ("dec dgrad cq", 8192, 512, 512, False, "R")]
+    for name, M, N, K, bk, epi in shapes:
         A = torch.randn(M, K, device="cuda").to(bf)
         W = (torch.randn(N, K, device="cuda") * 0.05).to(bf)
         Wm = W if bk else W.t().contiguous()
@@ -37,7 +46,7 @@ def main():
         for _ in range(5):
             ours.append(timeit(lambda: ops.gemm(A, Wm, M=M, N=N, K=K, b_kcontig=bk, out=C, **kw)))
             blas.append(timeit(lambda: torch.matmul(A, Wm.t() if bk else Wm)))
-        print("%-11s %-3s ours %7.1f us | blas %7.1f us   [%s]" % (name, epi, sorted(ours)[2], sorted(blas)[2], tag),
+        print("%-14s %-3s ours %7.1f us | blas %7.1f us   [%s]" % (name, epi, sorted(ours)[2], sorted(blas)[2], tag),
               flush=True)
         del A, W, Wm, X, C
         torch.cuda.empty_cache()
