@@ -727,14 +727,13 @@ def main():
                                                      "KV-cached), tokens/s")},
             "train_c4": c4 and {"metric": "C4 train tokens/s (B*(S+T)), 12+12 layers d768 h12, "
                                           "S=2048 T=512",
-                                "dtype": "fp8 (e4m3 forward GEMMs: QKV, attention out-"
-                                         "projections, FFN1, cross-attention Q and K/V; e4m3 "
-                                         "dgrads: FFN2, FFN1, out-projections, QKV, cross Q, "
-                                         "memory; e4m3 weight + bias gradients: QKV (layers >= 1), "
-                                         "out-projections, FFN1, cross Q and K/V; delayed "
-                                         "per-tensor scaling; attention, FFN2 forward and weight "
-                                         "gradient, first-layer QKV weight gradients and the "
-                                         "vocab head bf16)",
+                                "dtype": "fp8 (e4m3 forward GEMMs: QKV (layers >= 1), "
+                                         "attention out-projections, FFN1, FFN2, cross-attention "
+                                         "Q and K/V; e4m3 dgrads: FFN2, FFN1, out-projections, "
+                                         "QKV, cross Q, memory; e4m3 weight + bias gradients: "
+                                         "the same Linears; delayed per-tensor scaling; "
+                                         "attention, the first layers' QKV and the vocab head "
+                                         "bf16)",
                                 "value": round(c4["tokens_per_s"], 1),
                                 "ms_per_step": round(c4["ms_per_step"], 2),
                                 "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),

@@ -851,7 +851,9 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
       g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
     const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
     const int ch = tid & 31;
-#pragma unroll
+    // Q8: one item at a time (unrolled, the four items' temporaries beside
+    // the live accumulators spilled 42 VGPRs)
+#pragma unroll (Q8 ? 1 : 4)
     for (int c = 0; c < 4; ++c) {
       const int row = (tid >> 5) + 16 * c;
       const int grow = m0 + pass * 64 + row, gcol = n0 + ch * 8;
@@ -3623,7 +3625,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // FAST: bias columns
-    if (FAST && e.bias) {
+    // (Q8: loaded after the K loop, so its 8 registers are not live across it)
+    if (FAST && !Q8 && e.bias) {
       const float4 b0 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8);
       const float4 b1 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8 + 4);
       bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
@@ -3663,6 +3666,12 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
     __syncthreads();  // all fragment reads done before the epilogue reuses LDS
 
     if constexpr (FAST) {
+      if (Q8 && e.bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8);
+        const float4 b1 = *reinterpret_cast<const float4*>(e.bias + n0 + (tid & 31) * 8 + 4);
+        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
+        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+      }
       g2_fast_epilogue<Q8>(ee, acc, smem, m0, n0, tid, bv, xsrc, ldx, amax_acc);
       continue;
     }
@@ -4555,6 +4564,16 @@ extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, con
 // kernel trace: 133.5 vs 129.3 us at the 130-us shapes, 794 vs 698 at the
 // vocabulary-long K) and the step did not move (86.3 vs 85.9 ms), so the
 // two-stage kernel stays the default.
+// The e4m3-copy products (the gated FFN2 dgrad, FFN1 with SMER_FP8_FFN2)
+// on the streamed epilogue, whose residual / gate rows arrive by LDS-DMA a
+// pass ahead, one item at a time (round 6: C4 gated dgrad 65536 x 2048 x
+// 768 301 -> 245 us, step 78.96-78.99 -> 78.48-78.57 ms); SMER_FP8_Q8_FAST=0
+// (read per call) keeps the generic epilogue, whose gate loads are a
+// dependent HBM round trip per pass
+static bool smer_fp8_q8_fast() {
+  const char* e = getenv("SMER_FP8_Q8_FAST");
+  return !(e && e[0] == '0');
+}
 static bool smer_gemm256s_fp8_enabled(int K) {
   (void)K;
   const char* e = getenv("SMER_GEMM256S_FP8");
@@ -4631,7 +4650,16 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
   if (!e.vec)  // (q8 requires e.vec)
     hipLaunchKernelGGL((gemm256_fp8_kernel<false, false>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N,
                        K, (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
-  else if (q8)
+  else if (q8 && smer_fp8_q8_fast()) {
+    static bool attr_q = false;
+    if (!attr_q) {
+      hipFuncSetAttribute((const void*)gemm256_fp8_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          G2_LDS);
+      attr_q = true;
+    }
+    hipLaunchKernelGGL((gemm256_fp8_kernel<true, true>), dim3(grid), dim3(512), G2_LDS, s, M, N, K,
+                       (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  } else if (q8)
     hipLaunchKernelGGL((gemm256_fp8_kernel<false, true>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N, K,
                        (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
   else

@@ -41,11 +41,13 @@ class _W:
 
 
 # fp8 mode: FFN1 also writes the e4m3 copy of its ReLU output so that FFN2
-# runs on the fp8 MFMA too.  Measured at C4 (profiles/r02_c4_fp8_gemm.txt):
-# that extra 1-byte stream costs the FFN1 epilogue more (+76 us, 65536 x
-# 2048) than FFN2 gains over bf16 (-10 us: residual-bound epilogue), so by
-# default FFN1 runs fp8 with a bf16 output only and FFN2 stays bf16.
-FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "0") == "1"
+# runs on the fp8 MFMA too, forward and weight gradient.  Round 2 measured
+# that extra 1-byte stream costing the FFN1 epilogue more than FFN2 gained
+# (the e4m3-copy products then ran the generic epilogue, one dependent HBM
+# round trip per pass); round 6 moved them to the streamed epilogue and
+# made the weight gradients fp8: C4 78.24-78.31 -> 77.74-77.76 ms.
+# SMER_FP8_FFN2=0: FFN1 with a bf16 output only, FFN2 bf16 (A/B).
+FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "1") == "1"
 
 
 # Persistent-grid cap of the weight gradients on the side stream (workgroups;

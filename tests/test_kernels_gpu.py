@@ -1405,3 +1405,54 @@ def test_wgrad_fp8_declines_outside_tiling():
     one = torch.ones(1, device=dev)
     dw = torch.zeros(200, 200, device=dev)
     assert not O.linear_wgrad_fp8(z, one, z, one, dw)
+
+
+@pytest.mark.parametrize("mode", ["gate", "bias_relu_drop", "residual"])
+def test_fp8_q8_streamed_epilogue_equals_generic(monkeypatch, mode):
+    """The e4m3-copy fp8 products on the streamed epilogue (gate / residual
+    rows by LDS-DMA a pass ahead, the default) against the generic epilogue
+    (SMER_FP8_Q8_FAST=0).  Gate / residual: bf16 output, e4m3 copy and amax
+    bit for bit.  Bias + ReLU + dropout: the streamed epilogue fuses scale
+    and bias into one fma (the generic one rounds the product first), so
+    the outputs agree to a bf16 ulp and the same dropout zeros; in every
+    mode the copy is e4m3(out * qs) of the stored bf16 values exactly and
+    amax their max |out|."""
+    O = ops()
+    M, N, K = 512, 768, 768
+    g = torch.Generator(device="cpu").manual_seed(11)
+    A = torch.randint(-4, 5, (M, K), generator=g).float()
+    B = torch.randint(-3, 4, (N, K), generator=g).float()
+    a8 = A.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    b8 = B.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+    ai = torch.tensor([0.0123], device=dev)
+    bi = torch.tensor([0.37], device=dev)
+    X = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    qs = torch.tensor([37.0], device=dev)
+
+    def run(flag):
+        monkeypatch.setenv("SMER_FP8_Q8_FAST", flag)
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        am = torch.zeros(1, device=dev, dtype=torch.int32)
+        if mode == "gate":
+            assert O.gemm_fp8_ex(a8, ai, b8, bi, C, gate=X, gate_scale=1.25, q8=q, qs=qs, amax=am)
+        elif mode == "residual":
+            assert O.gemm_fp8_ex(a8, ai, b8, bi, C, residual=X, q8=q, qs=qs, amax=am)
+        else:
+            assert O.gemm_fp8_q(a8, ai, b8, bi, C, bias=bias, relu=True, drop_p=0.1, seed=5, q8=q, qs=qs,
+                                amax=am)
+        torch.cuda.synchronize()
+        return C.cpu(), q.cpu(), am.cpu()
+
+    fast, gen = run("1"), run("0")
+    C, q, am = fast
+    want_q = (C.float() * 37.0).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(q, want_q)
+    assert am.view(torch.float32).item() == C.float().abs().max().item()
+    if mode == "bias_relu_drop":
+        assert torch.equal(C == 0, gen[0] == 0)
+        torch.testing.assert_close(C.float(), gen[0].float(), rtol=2 ** -7, atol=0)
+    else:
+        for a, b in zip(fast, gen):
+            assert torch.equal(a, b)
