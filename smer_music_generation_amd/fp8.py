@@ -5,8 +5,8 @@ BASELINE.json configs[3] (C4) asks for fp8 MFMA GEMMs on CDNA4.  In the
 LayerNorm run on the block-scaled fp8 MFMA (`smer_gemm_fp8`): the QKV
 in-projections of layers >= 1, FFN1, the decoder's cross-attention Q and the
 stacked cross-attention K/V of the memory (`transformer.py:389,393,459,463,
-467`); FFN2 too when FFN1 writes an e4m3 copy of its output
-(engine.FP8_FFN2, off by default: measured slower at C4), and the attention
+467`); FFN2, whose input FFN1 writes in e4m3 beside its bf16 output
+(engine.FP8_FFN2, on since round 6), and the attention
 out-projections, whose input the attention forward writes in e4m3 beside O
 (FP8_ATTN_OUT).  The vocab head stays bf16; master weights fp32, working
 weights bf16.
@@ -24,8 +24,8 @@ is bf16).  W^T copies are quantised with the forward copies, once per
 optimizer step.  The memory dgrad (K = 12 * 2d) reads one e4m3 copy of
 every layer's cross-attention dK | dV under a single scale site (shared with
 the cross dQ copies).  Weight gradients (FP8_WGRAD, round 6): dW =
-e4m3(dY)^T e4m3(X) wherever both copies exist (every one but FFN2's, whose X
-copy needs engine.FP8_FFN2, and the first layers' QKV), through the
+e4m3(dY)^T e4m3(X) wherever both copies exist (all but the first layers'
+QKV, and FFN2's without engine.FP8_FFN2), through the
 transposing 8-bit LDS reads of smer_gemm_wgrad_fp8; the bias gradient from
 the same e4m3 dY.
 
