@@ -399,21 +399,23 @@ class Trainer:
         src, tin, tout = batch["input"], batch["target_in"], batch["target_out"]
         skpm, tkpm = batch["input_pad_mask"], batch["target_pad_mask"]
         B, T = tin.shape
-        with torch.no_grad():
-            logits, _, _ = eng.forward(src, tin, skpm, tkpm, skpm, training=False,
-                                       need_weights=False, save=False, seed=0)
-            y = tout.reshape(-1).contiguous().long()
-            denom = torch.empty(1, device=logits.device)
-            ops.wce_denom(y, self.ce_all, denom)
-            row_loss = torch.empty(B * T, device=logits.device)
-            loss = torch.empty(1, device=logits.device)
-            ops.wce_fwd_bwd(logits, y, self.w_total, denom, row_loss, loss, None, V=eng.V)
-            parts = self.loss_parts(row_loss, y, denom)
-            cls, names = self._class_table(logits.device)
-            counts = torch.zeros(2 * len(names) + 2, dtype=torch.int32, device=logits.device)
-            ops.argmax_accuracy(logits, y, cls, len(names), self.vocab.pad_index, counts)
-        if was_training:
-            model.train()
+        try:
+            with torch.no_grad():
+                logits, _, _ = eng.forward(src, tin, skpm, tkpm, skpm, training=False,
+                                           need_weights=False, save=False, seed=0)
+                y = tout.reshape(-1).contiguous().long()
+                denom = torch.empty(1, device=logits.device)
+                ops.wce_denom(y, self.ce_all, denom)
+                row_loss = torch.empty(B * T, device=logits.device)
+                loss = torch.empty(1, device=logits.device)
+                ops.wce_fwd_bwd(logits, y, self.w_total, denom, row_loss, loss, None, V=eng.V)
+                parts = self.loss_parts(row_loss, y, denom)
+                cls, names = self._class_table(logits.device)
+                counts = torch.zeros(2 * len(names) + 2, dtype=torch.int32, device=logits.device)
+                ops.argmax_accuracy(logits, y, cls, len(names), self.vocab.pad_index, counts)
+        finally:
+            if was_training:
+                model.train()
         return loss, parts, counts
 
     def accuracy_from_counts(self, counts):
