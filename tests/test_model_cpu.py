@@ -70,6 +70,28 @@ def test_abi_library_exports_every_header_symbol():
     assert lib.smer_abi_version() == 1
 
 
+def test_abi_round6_entry_points_validate_before_any_launch():
+    """The round-6 entry points reject what their tiling / contract cannot
+    take with the documented status and a message, before any HIP call (so
+    this runs without a GPU): smer_gemm_wgrad_fp8 returns
+    SMER_ERR_UNSUPPORTED (-3) off the 256 x 256 x 64 tiling, SMER_ERR_INVALID
+    (-1) for null operands; smer_argmax_accuracy rejects negative sizes."""
+    import ctypes
+    from smer_music_generation_amd import _lib
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * 64)()
+    p = ctypes.addressof(buf)
+    # M = 200: not a multiple of 256
+    assert lib.smer_gemm_wgrad_fp8(200, 256, 64, p, 256, p, 256, p, p, p, 256, 0, None, 0, None, 0, 0, None) == -3
+    assert b"256" in lib.smer_last_error()
+    # T = 100: not a multiple of 64
+    assert lib.smer_gemm_wgrad_fp8(256, 256, 100, p, 256, p, 256, p, p, p, 256, 0, None, 0, None, 0, 0, None) == -3
+    # null dy
+    assert lib.smer_gemm_wgrad_fp8(256, 256, 64, None, 256, p, 256, p, p, p, 256, 0, None, 0, None, 0, 0, None) == -1
+    assert lib.smer_argmax_accuracy(-1, 10, p, 10, p, p, 2, 0, p, None) == -1
+    assert lib.smer_argmax_accuracy(0, 10, p, 10, p, p, 2, 0, p, None) == 0  # no rows: nothing to do
+
+
 def test_data_library_exports_every_header_symbol():
     import ctypes
     hdr = open(os.path.join(ROOT, "include", "smer_data.h")).read()
