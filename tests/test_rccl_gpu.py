@@ -85,3 +85,44 @@ def test_rccl_world1_dp_step_equals_plain_step(nccl_group, monkeypatch, wire):
             assert torch.equal(g0.bfloat16().float(), g1), int((g0.bfloat16().float() != g1).sum())
     if wire == "fp32":
         assert torch.equal(m0.flat_parameters(), m1.flat_parameters())
+
+
+def test_rccl_world1_fp8_dp_step_equals_plain_step(nccl_group, monkeypatch):
+    """The fp8 step (e4m3 forward GEMMs, dgrads and weight gradients on the
+    side stream, whose e4m3 operands the hooks' all-reduces must not outrun)
+    over RCCL at world size 1 equals the plain fp8 step bit for bit, three
+    steps: the third runs every fp8 site on delayed scales (asserted through
+    the fp8 weight-gradient call count)."""
+    from smer_music_generation_amd import ops
+    from smer_music_generation_amd.model import ScoreTransformer
+    from smer_music_generation_amd.synth import synth_training_batch
+    from smer_music_generation_amd.train import Trainer
+    from smer_music_generation_amd.vocab import WordVocab
+    n_w8 = [0]
+    real = ops.linear_wgrad_fp8
+
+    def spy(*a, **kw):
+        r = real(*a, **kw)
+        n_w8[0] += int(bool(r))
+        return r
+    monkeypatch.setattr(ops, "linear_wgrad_fp8", spy)
+    v = WordVocab(0, ['key', 'tensile', 'density', 'polyphony', 'occupation'])
+
+    def make():
+        torch.manual_seed(0)
+        return ScoreTransformer(309, 512, 8, 2, 2, 2048, 2400, 0.1, 0.1, precision="fp8").to("cuda")
+    m0, m1 = make(), make()
+    b = synth_training_batch(78, v, 4, 1024, 256)
+    bt = {k: torch.from_numpy(np.asarray(x)).to("cuda") for k, x in b.items()}
+    plain = Trainer(m0, v, lr=1e-4)
+    dp = Trainer(m1, v, lr=1e-4, dp=True)
+    for k in range(3):
+        n_w8[0] = 0
+        l0 = plain.step(bt)
+        l1 = dp.step(bt)
+        torch.cuda.synchronize()
+        assert torch.equal(l0, l1), k
+        g0, g1 = m0.flat_grad(), m1.flat_grad()
+        assert torch.equal(g0, g1), "step %d: %d gradient elements differ" % (k, int((g0 != g1).sum()))
+    assert n_w8[0] > 0, "the third step ran no fp8 weight gradient"
+    assert torch.equal(m0.flat_parameters(), m1.flat_parameters())
