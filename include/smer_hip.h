@@ -366,6 +366,13 @@ int smer_layernorm_param_reduce(int M, int N, void* workspace, size_t ws_bytes, 
 int smer_embed_fwd(int dtype, int n_tok, int d, const int64_t* ids, const int32_t* positions,
                    int L, const float* table, const float* pe, float scale,
                    float drop_p, uint32_t seed, void* out, long ldo, smer_stream_t stream);
+/* smer_embed_fwd (bf16) plus the e4m3 copy q8 = e4m3(out * *qs) of the stored
+ * values, max |out| folded into *amax: the fp8 step's first-layer QKV input
+ * (transformer.py:389 after model.py:76, precision "fp8"; delayed scaling). */
+int smer_embed_fwd_fp8(int n_tok, int d, const int64_t* ids, const int32_t* positions, int L,
+                       const float* table, const float* pe, float scale, float drop_p, uint32_t seed,
+                       void* out, long ldo, void* q8, long ldq, const float* qs, unsigned* amax,
+                       smer_stream_t stream);
 size_t smer_embed_bwd_workspace(int V, int d, int n_tok_total);
 /* dtable[v] += scale * sum over both segments of dx[t] * keep/(1-p). */
 int smer_embed_bwd(int dtype, int V, int d, float scale,

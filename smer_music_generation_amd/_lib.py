@@ -28,6 +28,8 @@ SIGNATURES = {
     "smer_gemm_debug_stamps": (c_int, [P, c_size]),
     "smer_gemm_wgrad_bias": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,
                                      c_int, P, c_int, P, c_size, P]),
+    "smer_embed_fwd_fp8": (c_int, [c_int, c_int, P, P, c_int, P, P, c_float, c_float, c_u32, P, c_long, P, c_long,
+                                   P, P, P]),
     "smer_gemm_wgrad_fp8": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_long, c_int, P, c_int,
                                     P, c_size, c_int, P]),
     "smer_gemm_wgrad_bias_ex": (c_int, [c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long,

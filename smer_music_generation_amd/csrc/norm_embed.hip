@@ -403,28 +403,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
 // ---------------------------------------------------------------------------
 // embedding + sinusoidal PE
 // ---------------------------------------------------------------------------
-template <typename T>
+// Q8 (fp8 training, the first layers' QKV input): also the e4m3 copy
+// e4m3(out * *qs) of the stored bf16 values, max |out| folded into *amax
+// (delayed scaling, common.h)
+template <typename T, bool Q8 = false>
 __global__ void embed_fwd_kernel(int n_tok, int d, const int64_t* __restrict__ ids,
                                  const int32_t* __restrict__ positions, int L,
                                  const float* __restrict__ table, const float* __restrict__ pe,
                                  float scale, uint32_t thr, uint32_t seed, float dscale,
-                                 T* __restrict__ out, long ldo) {
+                                 T* __restrict__ out, long ldo, uint8_t* __restrict__ q8 = nullptr,
+                                 long ldq = 0, const float* __restrict__ qs_p = nullptr,
+                                 unsigned* __restrict__ amax = nullptr) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int per = d >> 2;
-  if (idx >= (long)n_tok * per) return;
-  int t = idx / per, c = (idx % per) * 4;
-  long id = ids[t];
-  int pos = positions ? positions[t] : t % L;
-  float4 e = *reinterpret_cast<const float4*>(table + id * d + c);
-  float4 p = *reinterpret_cast<const float4*>(pe + (long)pos * d + c);
-  float v[4] = {e.x * scale + p.x, e.y * scale + p.y, e.z * scale + p.z, e.w * scale + p.w};
-  T* o = out + (long)t * ldo + c;
+  const bool ok = idx < (long)n_tok * per;
+  if (!Q8 && !ok) return;  // (Q8: every lane reaches the wave-wide amax)
+  float am = 0.f;
+  if (ok) {
+    int t = idx / per, c = (idx % per) * 4;
+    long id = ids[t];
+    int pos = positions ? positions[t] : t % L;
+    float4 e = *reinterpret_cast<const float4*>(table + id * d + c);
+    float4 p = *reinterpret_cast<const float4*>(pe + (long)pos * d + c);
+    float v[4] = {e.x * scale + p.x, e.y * scale + p.y, e.z * scale + p.z, e.w * scale + p.w};
+    T* o = out + (long)t * ldo + c;
+    float f[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float w = v[i];
-    if (thr) w = smer_keep16(smer_rowkey(seed, (uint32_t)t), thr, (uint32_t)(c + i)) ? w * dscale : 0.f;
-    o[i] = from_f32<T>(w);
+    for (int i = 0; i < 4; ++i) {
+      float w = v[i];
+      if (thr) w = smer_keep16(smer_rowkey(seed, (uint32_t)t), thr, (uint32_t)(c + i)) ? w * dscale : 0.f;
+      const T ov = from_f32<T>(w);
+      o[i] = ov;
+      f[i] = to_f32(ov);
+    }
+    if constexpr (Q8) {
+      *reinterpret_cast<uint32_t*>(q8 + (long)t * ldq + c) = smer_q8x4(f, *qs_p);
+      am = smer_absmax4(f);
+    }
   }
+  if constexpr (Q8) smer_amax_commit(amax, am);
 }
 
 constexpr int EMB_CHUNK = 512;  // tokens per workgroup in the per-vocab gather
@@ -1021,6 +1038,24 @@ extern "C" int smer_embed_fwd(int dtype, int n_tok, int d, const int64_t* ids,
   else
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_embed_fwd: dtype");
   SMER_CHECK_LAUNCH("smer_embed_fwd");
+  return SMER_OK;
+}
+
+extern "C" int smer_embed_fwd_fp8(int n_tok, int d, const int64_t* ids, const int32_t* positions, int L,
+                                  const float* table, const float* pe, float scale, float drop_p,
+                                  uint32_t seed, void* out, long ldo, void* q8, long ldq, const float* qs,
+                                  unsigned* amax, smer_stream_t stream) {
+  SMER_REQUIRE(d % 4 == 0 && ldq % 4 == 0 && ((uintptr_t)q8 & 3) == 0, "smer_embed_fwd_fp8: d, ldq % 4 == 0");
+  SMER_REQUIRE(positions || L > 0, "smer_embed_fwd_fp8: L");
+  SMER_REQUIRE(ids && table && pe && out && q8 && qs && amax, "smer_embed_fwd_fp8: null pointer");
+  if (n_tok == 0) return SMER_OK;
+  hipStream_t s = (hipStream_t)stream;
+  long tot = (long)n_tok * (d / 4);
+  uint32_t thr = smer_drop_thr16(drop_p);
+  float ds = smer_drop_scale16(thr);
+  hipLaunchKernelGGL((embed_fwd_kernel<bf16, true>), dim3((tot + 255) / 256), dim3(256), 0, s, n_tok, d, ids,
+                     positions, L, table, pe, scale, thr, seed, ds, (bf16*)out, ldo, (uint8_t*)q8, ldq, qs, amax);
+  SMER_CHECK_LAUNCH("smer_embed_fwd_fp8");
   return SMER_OK;
 }
 

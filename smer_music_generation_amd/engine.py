@@ -48,6 +48,12 @@ class _W:
 # made the weight gradients fp8: C4 78.24-78.31 -> 77.74-77.76 ms.
 # SMER_FP8_FFN2=0: FFN1 with a bf16 output only, FFN2 bf16 (A/B).
 FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "1") == "1"
+# SMER_FP8_EMBED=1: the embedding also writes an e4m3 copy so that the first
+# encoder / decoder layers' QKV projections (forward, weight gradient) run
+# fp8 too.  Off: C4 79.54 vs 79.37 ms mean over 7 interleaved runs (noise
+# level) while the largest per-parameter gradient error of the C4 fp8 test
+# rose 0.564 -> 0.641 (decoder layer 0's norm1; bound 0.65).
+FP8_EMBED = os.environ.get("SMER_FP8_EMBED", "0") == "1"
 
 
 # Persistent-grid cap of the weight gradients on the side stream (workgroups;
@@ -260,6 +266,18 @@ class Engine:
         return y, mean, rstd, ((q, si) if f8.record_fwd(si) else None)
 
     @staticmethod
+    def _embed_q(f8, ids, table, pe, out, L, scale, p, seed, site):
+        """Embedding + PE; with f8 also its e4m3 copy for the first layer's
+        QKV projection: returns (copy, site) or None (as _ln_q)."""
+        if f8 is None or not FP8_EMBED or out.dtype != torch.bfloat16:
+            ops.embed(ids, table, pe, out, L=L, scale=scale, drop_p=p, seed=seed)
+            return None
+        si = f8.site(site)
+        q = torch.empty(out.shape, dtype=torch.uint8, device=out.device)
+        ops.embed_fp8(ids, table, pe, out, q, f8.qs_of(si), f8.amax_of(si), L=L, scale=scale, drop_p=p, seed=seed)
+        return (q, si) if f8.record_fwd(si) else None
+
+    @staticmethod
     def _attn_q8(f8, o, site, D):
         """fp8 forward: (q8 argument of ops.attn_fwd, (e4m3 copy of o, site)
         or None) so that the out-projection reads the attention output in
@@ -372,8 +390,8 @@ class Engine:
             f8.begin(W, training=training)
         ctx.f8 = f8 if (training and save) else None
         x = torch.empty(B * S, d, dtype=dt, device=dev)
-        ops.embed(src_ids, W.emb, pe2, x, L=S, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_src"]))
-        xq = None  # e4m3 copy of x (fp8 mode, layers >= 1)
+        # xq: e4m3 copy of each layer's input x (fp8 mode)
+        xq = self._embed_q(f8, src_ids, W.emb, pe2, x, S, math.sqrt(d), p_pos, sd(_SITE["pe_src"]), "emb.src")
         for i, L in enumerate(W.enc):
             xq_in = xq
             qkv = self._lin(f8, x, xq, "enc%d.in" % i, L.in_w, L.in_b)
@@ -402,11 +420,11 @@ class Engine:
         ctx.memq = memq
 
         y = torch.empty(B * T, d, dtype=dt, device=dev)
-        ops.embed(tgt_ids, W.emb, pe2, y, L=T, scale=math.sqrt(d), drop_p=p_pos, seed=sd(_SITE["pe_tgt"]))
+        yq0 = self._embed_q(f8, tgt_ids, W.emb, pe2, y, T, math.sqrt(d), p_pos, sd(_SITE["pe_tgt"]), "emb.tgt")
         wts = torch.empty(self.n_dec, B, T, S, device=dev) if need_weights else None
         # every decoder layer's cross-attention K|V of the memory, one GEMM
         kvc_all = self._lin(f8, mem, memq, "ckv", W.ckv_all, W.ckv_b_all) if self.n_dec else None
-        yq = None
+        yq = yq0
         for i, L in enumerate(W.dec):
             yq_in = yq
             qkv = self._lin(f8, y, yq, "dec%d.sa" % i, L.sa_w, L.sa_b)

@@ -677,6 +677,15 @@ def embed(ids, table, pe, out, *, L=0, positions=None, scale, drop_p=0.0, seed=0
          _ld(out), _stream())
 
 
+def embed_fp8(ids, table, pe, out, q8, qs, amax, *, L=0, positions=None, scale, drop_p=0.0, seed=0):
+    """embed (bf16 out) plus the e4m3 copy q8 = e4m3(out * qs), max |out|
+    folded into amax (the fp8 step's first-layer QKV input)."""
+    n_tok = ids.numel()
+    d = table.shape[1]
+    call("smer_embed_fwd_fp8", n_tok, d, _p(ids), _p(positions), int(L), _p(table), _p(pe), float(scale),
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out), _p(q8), _ld(q8), _p(qs), _p(amax), _stream())
+
+
 def embed_bwd(dtable, scale, segs):
     """segs: list of up to two (ids int64 [n], dx [n, d], drop_p, seed)."""
     lib = load()

@@ -1456,3 +1456,27 @@ def test_fp8_q8_streamed_epilogue_equals_generic(monkeypatch, mode):
     else:
         for a, b in zip(fast, gen):
             assert torch.equal(a, b)
+
+
+def test_embed_fp8_copy_matches_embed():
+    """smer_embed_fwd_fp8: the same bf16 output as smer_embed_fwd (with
+    positional dropout), its e4m3 copy e4m3(out * qs) of the stored values
+    and amax = max |out| (the fp8 step's first-layer QKV input)."""
+    O = ops()
+    V, d, B, L = 309, 512, 3, 200
+    g = torch.Generator(device="cpu").manual_seed(21)
+    table = torch.randn(V, d, generator=g).to(dev)
+    pe = torch.randn(4096, d, generator=g).to(dev)
+    ids = torch.randint(0, V, (B * L,), generator=g).to(dev)
+    a = torch.empty(B * L, d, device=dev, dtype=torch.bfloat16)
+    b = torch.empty_like(a)
+    q = torch.empty(B * L, d, device=dev, dtype=torch.uint8)
+    qs = torch.tensor([20.0], device=dev)
+    am = torch.zeros(1, device=dev, dtype=torch.int32)
+    O.embed(ids, table, pe, a, L=L, scale=22.6, drop_p=0.1, seed=5)
+    O.embed_fp8(ids, table, pe, b, q, qs, am, L=L, scale=22.6, drop_p=0.1, seed=5)
+    torch.cuda.synchronize()
+    assert torch.equal(a.cpu(), b.cpu())
+    want = (b.float().cpu() * 20.0).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(q.cpu(), want)
+    assert am.cpu().view(torch.float32).item() == b.float().abs().max().item()
