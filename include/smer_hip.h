@@ -448,7 +448,8 @@ int smer_gemm_fp8(int M, int N, int K, const void* A, long lda, const void* B, l
  * an e4m3 copy q8 = e4m3(out * *qs) beside their bf16 output and fold
  * max|out| into *amax (float bits, atomicMax); qs / inv come from the
  * previous step's amax via smer_fp8_scales.  smer_gemm_fp8_q is
- * smer_gemm_fp8 plus such a copy of C (the FFN1 output feeding FFN2);
+ * smer_gemm_fp8 plus such a copy of C (the FFN1 output feeding FFN2; C may
+ * be null on the streamed epilogue, SMER_FP8_Q8_FAST, to write the copy alone);
  * smer_layernorm_fwd_fp8 is smer_layernorm_fwd (bf16) plus such a copy of y.
  * smer_fp8_scales: for i < n, qs[i] = 448 / amax_prev[i], inv[i] =
  * amax_prev[i] / 448 (both 1 when amax_prev is 0), amax_next[i] = 0. */
@@ -484,6 +485,15 @@ int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, const void* B
                      const void* residual, long ldr, const void* gate, long ldg, float gate_scale,
                      float drop_p, uint32_t drop_seed, void* C, long ldc, void* q8, long ldq8,
                      const float* qs, unsigned* amax, smer_stream_t stream);
+/* smer_gemm_fp8_ex's gated product (the FFN2 dgrad, transformer.py:467-469
+ * under train.py:783) with the gate read from FFN1's e4m3 copy: out = gate
+ * byte a positive nonzero e4m3 ? v * gate_scale : 0, plus the e4m3 copy of
+ * out (q8 required; 16-B aligned gate rows, ldg % 16 == 0).  With it FFN1
+ * may write its e4m3 copy alone (smer_gemm_fp8_q with C null). */
+int smer_gemm_fp8_gate8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                        const float* a_inv, const float* b_inv, const void* gate8, long ldg,
+                        float gate_scale, void* C, long ldc, void* q8, long ldq8, const float* q8_scale,
+                        unsigned* q8_amax, smer_stream_t stream);
 int smer_layernorm_bwd_fp8(int M, int N, const void* dy, long lddy, const void* x, long ldx,
                            const float* mean, const float* rstd, const float* gamma, void* dx,
                            long lddx, void* dx_drop, long ldxd, float drop_p, uint32_t seed,

@@ -88,6 +88,8 @@ SIGNATURES = {
     "smer_fp8_quantize_segments_t": (c_int, [c_int, P, P, P, c_int, P]),
     "smer_gemm_fp8_ex": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_int, P, c_long,
                                  P, c_long, c_float, c_float, c_u32, P, c_long, P, c_long, P, P, P]),
+    "smer_gemm_fp8_gate8": (c_int, [c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, c_long, c_float,
+                                    P, c_long, P, c_long, P, P, P]),
     "smer_layernorm_bwd_fp8": (c_int, [c_int, c_int, P, c_long, P, c_long, P, P, P, P, c_long, P, c_long,
                                        c_float, c_u32, P, c_long, P, P, P, P, c_int, P, c_size, c_int,
                                        P]),

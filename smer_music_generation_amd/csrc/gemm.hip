@@ -754,10 +754,25 @@ constexpr int G2_LDS = G2_XA + 64 * G2 * 2;         // 160 KiB total
 
 // 64 rows x 256 bf16 columns of X (row-major, ld) -> LDS [64][512 B], by
 // LDS-DMA: wave w's instruction c fills 1 KiB = rows 2(4w+c), +1.
-__device__ __forceinline__ void g2_xload(char* dst, const bf16* X, long ld, int r0, int c0, int tid) {
+// G8: 64 rows x 256 byte columns (an e4m3 gate) -> LDS [64][256 B]: wave w's
+// instruction c fills rows 4(2w+c) .. +3.
+__device__ __forceinline__ void g2_xload(char* dst, const void* Xv, long ld, int r0, int c0, int tid,
+                                         bool g8 = false) {
   typedef __attribute__((address_space(1))) void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   const int lane = tid & 63, wave = tid >> 6;
+  if (g8) {
+    const uint8_t* X8 = (const uint8_t*)Xv;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int chunk = wave * 2 + c;
+      const int row = chunk * 4 + (lane >> 4);
+      const uint8_t* src = X8 + (long)(r0 + row) * ld + c0 + (lane & 15) * 16;
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + chunk * 1024), 16, 0, 0);
+    }
+    return;
+  }
+  const bf16* X = (const bf16*)Xv;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int chunk = wave * 4 + c;
@@ -818,10 +833,13 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int
 // each; the bias is in registers (a thread always owns the same 8 columns).
 // The caller DMA'd the X rows of pass 0 into slot A during its K loop.
 // Q8: also the e4m3 copy of the stored values (fp8 training forward).
-template <bool Q8>
+// G8: the gate is an e4m3 copy (a template flag: a runtime read of it from
+// the kernel arguments is a scalar load the compiler may place inside the
+// k-loop, where it upsets the loop's counted lgkmcnt waits)
+template <bool Q8, bool G8 = false>
 __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (&acc)[8][4], char* smem,
                                                  int m0, int n0, int tid, const float (&bv)[8],
-                                                 const bf16* xsrc, long ldx, float& amax_acc) {
+                                                 const void* xsrc, long ldx, float& amax_acc) {
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int g = lane >> 4, c16 = lane & 15;
@@ -829,7 +847,8 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
   float* ep = reinterpret_cast<float*>(smem);
   float q8s = 1.f;
   if constexpr (Q8) q8s = *e.q8_scale;
-  if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid);
+  constexpr bool g8 = G8;
+  if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid, g8);
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     if (wm == (pass >> 1)) {
@@ -848,7 +867,7 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
     if (xsrc) __syncthreads();
     else smer_lds_barrier();
     if (xsrc && pass >= 1 && pass < 3)
-      g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
+      g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid, g8);
     const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
     const int ch = tid & 31;
     // Q8: one item at a time (unrolled, the four items' temporaries beside
@@ -869,7 +888,14 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
       }
       if (e.drop_thr)
         smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
-      if (xsrc) {
+      if (xsrc && g8) {
+        const uint2 gb = *reinterpret_cast<const uint2*>(xs + row * 256 + ch * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t byte = ((k < 4 ? gb.x : gb.y) >> (8 * (k & 3))) & 0xffu;
+          v[k] = byte - 1u < 0x7fu ? v[k] * e.gate_scale : 0.f;  // 1..127: positive
+        }
+      } else if (xsrc) {
         const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xs + row * 512 + ch * 16);
         if (e.residual) {
 #pragma unroll
@@ -882,7 +908,8 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
       bf16x8 o;
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-      *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+      if (!Q8 || e.C)  // (Q8: the e4m3 copy alone when C is null)
+        *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
       if constexpr (Q8) {  // e4m3 copy of the stored (bf16-rounded) values
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = (float)o[k];
@@ -3584,7 +3611,7 @@ __device__ __forceinline__ void f8_kstep(f32x4 (&acc)[8][4], i32x8 (&af)[8], i32
 // FAST: the streamed epilogue (e.vec: 16-B aligned vectors; LDS G2_LDS);
 // Q8: also write the e4m3 copy of the output (launched with the generic
 // epilogue: the streamed one spills 37 VGPRs with it and measured slower).
-template <bool FAST, bool Q8>
+template <bool FAST, bool Q8, bool G8 = false>
 __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K,
                                                              const uint8_t* __restrict__ A, long lda,
                                                              const uint8_t* __restrict__ B, long ldb,
@@ -3606,7 +3633,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   GemmEpi ee = e;
   ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
   float amax_acc = 0.f;
-  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);  // streamed epilogue operand
+  const void* xsrc = e.residual ? e.residual : e.gate;  // streamed epilogue operand
   const long ldx = e.residual ? e.ldr : e.ldg;
   g2_start_skew(e.skew);
 
@@ -3637,7 +3664,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // stage kt landed; stage kt-1 fully read
       // X rows of the first epilogue pass into slot A (beyond the stages)
-      if (FAST && xsrc && kt == nk / 2) g2_xload(smem + G2_XA, xsrc, ldx, m0, n0, tid);
+      if (FAST && xsrc && kt == nk / 2) g2_xload(smem + G2_XA, xsrc, ldx, m0, n0, tid, G8);
       if (kt + 1 < nk) {
         char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
         f8_glds(nb, A, lda, M, m0, (kt + 1) * F8K, tid);
@@ -3672,7 +3699,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
         bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
         bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
       }
-      g2_fast_epilogue<Q8>(ee, acc, smem, m0, n0, tid, bv, xsrc, ldx, amax_acc);
+      g2_fast_epilogue<Q8, G8>(ee, acc, smem, m0, n0, tid, bv, xsrc, ldx, amax_acc);
       continue;
     }
     const int g = lane >> 4, c16 = lane & 15;
@@ -4597,15 +4624,20 @@ extern "C" int smer_gemm_fp8_q(int M, int N, int K, const void* A, long lda, con
                           drop_p, drop_seed, C, ldc, q8, ldq8, q8_scale, q8_amax, stream);
 }
 
-extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                                const float* a_inv, const float* b_inv, const float* bias, int relu,
-                                const void* residual, long ldr, const void* gate, long ldg,
-                                float gate_scale, float drop_p, uint32_t drop_seed, void* C, long ldc,
-                                void* q8, long ldq8, const float* q8_scale, unsigned* q8_amax,
-                                smer_stream_t stream) {
+static int gemm_fp8_impl(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                         const float* a_inv, const float* b_inv, const float* bias, int relu,
+                         const void* residual, long ldr, const void* gate, long ldg, int gate_u8,
+                         float gate_scale, float drop_p, uint32_t drop_seed, void* C, long ldc,
+                         void* q8, long ldq8, const float* q8_scale, unsigned* q8_amax,
+                         smer_stream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % G2 || N % G2 || K % F8K)
     return smer_set_error(SMER_ERR_UNSUPPORTED, "smer_gemm_fp8: needs M, N % 256 == 0 and K % 128 == 0");
-  SMER_REQUIRE(A && B && C && a_inv && b_inv, "smer_gemm_fp8: null pointer");
+  // (C may be null only beside an e4m3 copy on the streamed epilogue: the
+  // copy alone is written)
+  const bool c_less = !C && q8 && smer_fp8_q8_fast();
+  SMER_REQUIRE(A && B && (C || c_less) && a_inv && b_inv, "smer_gemm_fp8: null pointer");
+  SMER_REQUIRE(!gate_u8 || (gate && q8 && smer_fp8_q8_fast() && ((uintptr_t)gate & 15) == 0 && ldg % 16 == 0),
+               "smer_gemm_fp8_gate8: e4m3 gate needs the streamed e4m3-copy epilogue and 16-B aligned rows");
   SMER_REQUIRE(lda % 16 == 0 && ldb % 16 == 0 && aligned16(A) && aligned16(B),
                "smer_gemm_fp8: operand strides / alignment");
   SMER_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "smer_gemm_fp8: drop_p out of range");
@@ -4618,6 +4650,7 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
   SMER_REQUIRE(!(gate && residual), "smer_gemm_fp8_ex: residual and gate are exclusive");
   auto a16 = [](const void* p, long ld) { return p == nullptr || ((((uintptr_t)p) & 15) == 0 && ld % 8 == 0); };
   e.vec = a16(bias, 8) && a16(residual, ldr) && a16(gate, ldg) && a16(C, ldc);
+  SMER_REQUIRE((C && !gate_u8) || e.vec, "smer_gemm_fp8: the e4m3-only output and the e4m3 gate need aligned vectors");
   if (q8) {
     SMER_REQUIRE(e.vec && q8_scale && q8_amax && (((uintptr_t)q8) & 7) == 0 && ldq8 % 8 == 0,
                  "smer_gemm_fp8_q: fp8 output needs aligned vectors, scale and amax");
@@ -4650,7 +4683,16 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
   if (!e.vec)  // (q8 requires e.vec)
     hipLaunchKernelGGL((gemm256_fp8_kernel<false, false>), dim3(grid), dim3(512), 2 * G2_STAGE, s, M, N,
                        K, (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
-  else if (q8 && smer_fp8_q8_fast()) {
+  else if (gate_u8) {
+    static bool attr_g8 = false;
+    if (!attr_g8) {
+      hipFuncSetAttribute((const void*)gemm256_fp8_kernel<true, true, true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+      attr_g8 = true;
+    }
+    hipLaunchKernelGGL((gemm256_fp8_kernel<true, true, true>), dim3(grid), dim3(512), G2_LDS, s, M, N, K,
+                       (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
+  } else if (q8 && smer_fp8_q8_fast()) {
     static bool attr_q = false;
     if (!attr_q) {
       hipFuncSetAttribute((const void*)gemm256_fp8_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4667,4 +4709,25 @@ extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, co
                        (const uint8_t*)A, lda, (const uint8_t*)B, ldb, a_inv, b_inv, e);
   SMER_CHECK_LAUNCH("smer_gemm_fp8");
   return SMER_OK;
+}
+
+extern "C" int smer_gemm_fp8_ex(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                                const float* a_inv, const float* b_inv, const float* bias, int relu,
+                                const void* residual, long ldr, const void* gate, long ldg,
+                                float gate_scale, float drop_p, uint32_t drop_seed, void* C, long ldc,
+                                void* q8, long ldq8, const float* q8_scale, unsigned* q8_amax,
+                                smer_stream_t stream) {
+  return gemm_fp8_impl(M, N, K, A, lda, B, ldb, a_inv, b_inv, bias, relu, residual, ldr, gate, ldg, 0,
+                       gate_scale, drop_p, drop_seed, C, ldc, q8, ldq8, q8_scale, q8_amax, stream);
+}
+
+// The gated FFN2 dgrad of the fp8 step with FFN1's e4m3 copy as the ReLU /
+// dropout gate (open where the byte is a positive nonzero e4m3), so FFN1
+// need not keep its bf16 output (transformer.py:467-469 under train.py:783).
+extern "C" int smer_gemm_fp8_gate8(int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                                   const float* a_inv, const float* b_inv, const void* gate8, long ldg,
+                                   float gate_scale, void* C, long ldc, void* q8, long ldq8,
+                                   const float* q8_scale, unsigned* q8_amax, smer_stream_t stream) {
+  return gemm_fp8_impl(M, N, K, A, lda, B, ldb, a_inv, b_inv, nullptr, 0, nullptr, 0, gate8, ldg, 1,
+                       gate_scale, 0.f, 0u, C, ldc, q8, ldq8, q8_scale, q8_amax, stream);
 }

@@ -54,6 +54,12 @@ FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "1") == "1"
 # level) while the largest per-parameter gradient error of the C4 fp8 test
 # rose 0.564 -> 0.641 (decoder layer 0's norm1; bound 0.65).
 FP8_EMBED = os.environ.get("SMER_FP8_EMBED", "0") == "1"
+# SMER_FP8_H8=1: once FFN1's e4m3 copy feeds FFN2 (its site has a scale
+# history), FFN1 writes that copy alone, and the FFN2 dgrad takes its ReLU /
+# dropout gate from the copy (smer_gemm_fp8_gate8): no bf16 [tokens, F]
+# activation is written or read back.  Needs the streamed e4m3-copy epilogue.
+FP8_H8 = (os.environ.get("SMER_FP8_H8", "1") == "1"
+          and os.environ.get("SMER_FP8_Q8_FAST", "1") != "0")
 
 
 # Persistent-grid cap of the weight gradients on the side stream (workgroups;
@@ -278,6 +284,21 @@ class Engine:
         return (q, si) if f8.record_fwd(si) else None
 
     @staticmethod
+    def _deq8(hq, f8):
+        """bf16 values of an e4m3 copy (q, site) (a bf16 fallback's input
+        when FFN1 kept only its copy; not on the fp8 step's path)."""
+        return (hq[0].view(torch.float8_e4m3fn).float() * f8.inv_of(hq[1])).to(torch.bfloat16)
+
+    @staticmethod
+    def _ffn2_fp8(f8, M, w2, name):
+        """Whether FFN2 (w2 [d, F]) runs on the fp8 MFMA whenever its input
+        has a usable e4m3 copy (then FFN1 may write that copy alone)."""
+        if f8 is None:
+            return False
+        from .fp8 import FWD_GROUPS, eligible, fwd_group
+        return eligible(M, w2.shape[0], w2.shape[1]) and fwd_group(name) in FWD_GROUPS
+
+    @staticmethod
     def _attn_q8(f8, o, site, D):
         """fp8 forward: (q8 argument of ops.attn_fwd, (e4m3 copy of o, site)
         or None) so that the out-projection reads the attention output in
@@ -290,28 +311,35 @@ class Engine:
         q = torch.empty(o.shape, dtype=torch.uint8, device=o.device)
         return (q, f8.qs_of(si), f8.amax_of(si)), ((q, si) if f8.record_fwd(si) else None)
 
-    def _lin(self, f8, x, xq, wname, w, b, q_site=None, **epi):
+    def _lin(self, f8, x, xq, wname, w, b, q_site=None, q_only=False, **epi):
         """x @ w^T + epilogue: on the fp8 MFMA when x has an e4m3 copy xq and
         the shape tiles, else bf16.  q_site: also write the e4m3 copy of the
         output (returns (out, (q, site)) — (out, None) when the FFN2 input
-        copy is disabled, see FP8_FFN2)."""
-        M, K = x.shape
+        copy is disabled, see FP8_FFN2).  q_only: the consumer runs fp8
+        whenever the copy is usable, so then only the copy is written and out
+        is None (FP8_H8)."""
+        M, K = (x if x is not None else xq[0]).shape  # (x None: only the e4m3 copy exists)
         N = w.shape[0]
+        adt, adev = (x.dtype, x.device) if x is not None else (torch.bfloat16, xq[0].device)
         if q_site is not None and not FP8_FFN2:
             return self._lin(f8, x, xq, wname, w, b, **epi), None
         if f8 is not None and xq is not None:
             from .fp8 import FWD_GROUPS, eligible, fwd_group
             if eligible(M, N, K) and epi.get("gate") is None and fwd_group(wname) in FWD_GROUPS:
                 w8, winv = f8.weight(wname, w)
-                out = torch.empty(M, N, dtype=x.dtype, device=x.device)
                 if q_site is not None:
                     si = f8.site(q_site)
-                    q = torch.empty(M, N, dtype=torch.uint8, device=x.device)
+                    out = None if (q_only and FP8_H8 and si in f8.fwd_ready) else \
+                        torch.empty(M, N, dtype=adt, device=adev)
+                    q = torch.empty(M, N, dtype=torch.uint8, device=adev)
                     ops.gemm_fp8_q(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, q8=q,
                                    qs=f8.qs_of(si), amax=f8.amax_of(si), **epi)
                     return out, ((q, si) if f8.record_fwd(si) else None)
+                out = torch.empty(M, N, dtype=adt, device=adev)
                 ops.gemm_fp8(xq[0], f8.inv_of(xq[1]), w8, winv, out, bias=b, **epi)
                 return out
+        if x is None:
+            raise RuntimeError("engine: %s has only an e4m3 input but did not run fp8" % wname)
         out = ops.linear(x, w, b, **epi)
         return (out, None) if q_site is not None else out
 
@@ -405,6 +433,7 @@ class Engine:
                            seed=sd(_site("enc", i, 1)))
             x1, m1, r1, x1q = self._ln_q(f8, y1, L.n1, dt, "enc%d.ln1" % i)
             h, hq = self._lin(f8, x1, x1q, "enc%d.l1" % i, L.l1_w, L.l1_b, q_site="enc%d.h" % i,
+                              q_only=self._ffn2_fp8(f8, B * S, L.l2_w, "enc%d.l2" % i),
                               relu=True, drop_p=p_tr, seed=sd(_site("enc", i, 2)))
             y2 = self._lin(f8, h, hq, "enc%d.l2" % i, L.l2_w, L.l2_b, residual=x1, drop_p=p_tr,
                            seed=sd(_site("enc", i, 3)))
@@ -452,6 +481,7 @@ class Engine:
                            seed=sd(_site("dec", i, 3)))
             x2, m2, r2, x2q = self._ln_q(f8, y2, L.n2, dt, "dec%d.ln2" % i)
             h, hq = self._lin(f8, x2, x2q, "dec%d.l1" % i, L.l1_w, L.l1_b, q_site="dec%d.h" % i,
+                              q_only=self._ffn2_fp8(f8, B * T, L.l2_w, "dec%d.l2" % i),
                               relu=True, drop_p=p_tr, seed=sd(_site("dec", i, 4)))
             y3 = self._lin(f8, h, hq, "dec%d.l2" % i, L.l2_w, L.l2_b, residual=x2, drop_p=p_tr,
                            seed=sd(_site("dec", i, 5)))
@@ -499,6 +529,8 @@ class Engine:
                                                        accumulate=kw.get("accumulate", True), ws=ws,
                                                        max_wg=cap):
                 return
+            if x is None:
+                raise RuntimeError("engine: fp8 weight gradient declined with no bf16 input")
             ops.linear_wgrad(dy, x, gw, ws=ws, max_wg=cap, **kw)
         if side is None:
             run(None, 0)
@@ -515,7 +547,8 @@ class Engine:
         # temporaries freed on the main stream must not be reused before the
         # side stream has read them
         dy.record_stream(stream)
-        x.record_stream(stream)
+        if x is not None:
+            x.record_stream(stream)
         if q8 is not None:
             q8[0].record_stream(stream)
             q8[2].record_stream(stream)
@@ -628,6 +661,29 @@ class Engine:
             if f8w is not None and dyq is not None and xq is not None:
                 kw["q8"] = (dyq[0], f8w.inv_of(dyq[1]), xq[0], f8w.inv_of(xq[1]))
             wg_(dy_, x_, gw, **kw)
+        def ffn2_bwd(dyq, dyd, name, w2, GL, h, hq, q_site):
+            """FFN2's weight gradient and gated dgrad (returns dh, its e4m3
+            copy).  h None: FFN1 kept only its e4m3 copy hq (FP8_H8); the gate
+            then comes from the copy (smer_gemm_fp8_gate8), and bf16 values
+            are rebuilt from it only where a bf16 fallback needs them."""
+            gs = ops.drop_scale(p_tr)
+            if h is None and not (f8 is not None and f8w is not None and dyq is not None
+                                  and f8.weight_t(name) is not None):
+                h = self._deq8(hq, ctx.f8)
+            wg(dyd, h, GL.l2_w, dyq, hq, db=GL.l2_b)
+            if h is not None:
+                return dgrad(dyq, dyd, name, w2, q_site=q_site, gate=h, gate_scale=gs)
+            wt = f8.weight_t(name)
+            si = f8.site(q_site)
+            M, N = dyd.shape[0], w2.shape[1]
+            out = torch.empty(M, N, dtype=dt, device=dev)
+            q = torch.empty(M, N, dtype=torch.uint8, device=dev)
+            if not ops.gemm_fp8_gate8(dyq[0], f8.inv_of(dyq[1]), wt[0], wt[1], hq[0], gs, out, q,
+                                      f8.qs_of(si), f8.amax_of(si)):
+                raise RuntimeError("engine: %s e4m3-gated dgrad declined its shape" % name)
+            f8.record_bwd(q_site)
+            return out, ((q, si) if q_site in f8.bwd_ready else None)
+
         ops.ck("M:dlog", dlog_pad)
         wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
         g_out = ops.linear_dgrad(dlog_pad, W.fc_pad, K=self.Vp)
@@ -659,9 +715,7 @@ class Engine:
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
             ck("M:dec%d.dy3" % i, dy3d)
-            wg(dy3d, h, GL.l2_w, dy3q, hq, db=GL.l2_b)
-            dh, dhq = dgrad(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, q_site="b.dec%d.dh" % i, gate=h,
-                            gate_scale=ops.drop_scale(p_tr))
+            dh, dhq = ffn2_bwd(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, GL, h, hq, "b.dec%d.dh" % i)
             ck("M:dec%d.dh" % i, dh)
             wg(dh, x2, GL.l1_w, dhq, x2q, db=GL.l1_b)
             dx2, _ = dgrad(dhq, dh, "dec%d.l1" % i, L.l1_w, residual=dy3)
@@ -742,9 +796,7 @@ class Engine:
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
             ck("M:enc%d.dy2" % i, dy2d)
-            wg(dy2d, h, GL.l2_w, dy2q, hq, db=GL.l2_b)
-            dh, dhq = dgrad(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, q_site="b.enc%d.dh" % i, gate=h,
-                            gate_scale=ops.drop_scale(p_tr))
+            dh, dhq = ffn2_bwd(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, GL, h, hq, "b.enc%d.dh" % i)
             ck("M:enc%d.dh" % i, dh)
             wg(dh, x1, GL.l1_w, dhq, x1q, db=GL.l1_b)
             dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)

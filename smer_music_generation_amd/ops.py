@@ -526,10 +526,34 @@ def gemm_fp8(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None,
     return True
 
 
+def gemm_fp8_gate8(a8, a_inv, b8, b_inv, gate8, gate_scale, out, q8, qs, amax):
+    """out[M,N] bf16 = gate8 > 0 ? a_inv*b_inv * (a8 @ b8^T) * gate_scale : 0
+    with the gate read from an e4m3 copy (bytes 1..127 open), plus the e4m3
+    copy of out: the fp8 step's FFN2 dgrad when FFN1 kept only its e4m3
+    output.  Returns False (nothing launched) outside the tiling."""
+    M, K = a8.shape
+    N = b8.shape[0]
+    if M % 256 or N % 256 or K % 128:
+        return False
+    timer = GEMM_TIMER
+    if timer is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    call("smer_gemm_fp8_gate8", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
+         _p(gate8), _ld(gate8), float(gate_scale), _p(out), _ld(out), _p(q8), _ld(q8), _p(qs), _p(amax),
+         _stream())
+    if timer is not None:
+        ev1.record()
+        timer.records.append((ev0, ev1, 2.0 * M * N * K, "fp8 dgrad M%d N%d K%d g8" % (M, N, K)))
+    return True
+
+
 def gemm_fp8_q(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=None, drop_p=0.0,
                seed=0, q8=None, qs=None, amax=None):
     """gemm_fp8 plus an e4m3 copy of `out` (q8 = e4m3(out * qs), max|out| folded
-    into amax): the fp8 training forward's FFN1 (its output feeds FFN2)."""
+    into amax): the fp8 training forward's FFN1 (its output feeds FFN2).
+    out=None: the e4m3 copy alone (streamed epilogue, SMER_FP8_Q8_FAST)."""
     M, K = a8.shape
     N = b8.shape[0]
     if M % 256 or N % 256 or K % 128:
@@ -541,7 +565,7 @@ def gemm_fp8_q(a8, a_inv, b8, b_inv, out, *, bias=None, relu=False, residual=Non
         ev0.record()
     call("smer_gemm_fp8_q", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
          _p(bias), int(bool(relu)), _p(residual), _ld(residual) if residual is not None else 0,
-         float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out), _p(q8),
+         float(drop_p), int(seed) & 0xFFFFFFFF, _p(out), _ld(out) if out is not None else 0, _p(q8),
          _ld(q8) if q8 is not None else 0, _p(qs), _p(amax), _stream())
     if timer is not None:
         ev1.record()

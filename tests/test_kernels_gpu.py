@@ -1480,3 +1480,49 @@ def test_embed_fp8_copy_matches_embed():
     want = (b.float().cpu() * 20.0).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
     assert torch.equal(q.cpu(), want)
     assert am.cpu().view(torch.float32).item() == b.float().abs().max().item()
+
+
+def test_fp8_e4m3_gate_and_copy_only_output():
+    """smer_gemm_fp8_gate8 (the FFN2 dgrad gated by FFN1's e4m3 copy) equals
+    smer_gemm_fp8_ex gated by the copy's dequantised bf16 values bit for bit
+    (output, e4m3 copy, amax), and smer_gemm_fp8_q with a null C writes the
+    same e4m3 copy and amax as with C."""
+    O = ops()
+    M, N, K = 512, 768, 256
+    g = torch.Generator(device="cpu").manual_seed(8)
+    e4 = lambda t: t.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)  # noqa: E731
+    a8, b8 = e4(torch.randn(M, K, generator=g) * 4), e4(torch.randn(N, K, generator=g) * 4)
+    inv = torch.tensor([1.0 / 32], device=dev)
+    # the gate: an e4m3 copy with zeros, negative zeros, negatives and positives
+    gq = torch.randn(M, N, generator=g) * 3
+    gq[torch.rand(M, N, generator=g) < 0.2] = 0.0
+    gq[torch.rand(M, N, generator=g) < 0.05] = -0.0
+    g8 = e4(gq)
+    g_bf = g8.view(torch.float8_e4m3fn).float().mul(0.25).to(torch.bfloat16)
+    qs = torch.tensor([3.0], device=dev)
+    outs = []
+    for use8 in (False, True):
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        am = torch.zeros(1, device=dev, dtype=torch.int32)
+        if use8:
+            assert O.gemm_fp8_gate8(a8, inv, b8, inv, g8, 1.25, out, q, qs, am)
+        else:
+            assert O.gemm_fp8_ex(a8, inv, b8, inv, out, gate=g_bf, gate_scale=1.25, q8=q, qs=qs, amax=am)
+        outs.append((out, q, am))
+    torch.cuda.synchronize()
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x.cpu(), y.cpu())
+    assert int((outs[1][0] == 0).sum()) > M * N // 5  # the gate closed somewhere
+    # FFN1 with and without its bf16 output
+    bias = torch.randn(N, generator=g).to(dev)
+    res = []
+    for with_c in (True, False):
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if with_c else None
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        am = torch.zeros(1, device=dev, dtype=torch.int32)
+        assert O.gemm_fp8_q(a8, inv, b8, inv, out, bias=bias, relu=True, drop_p=0.1, seed=4, q8=q, qs=qs,
+                            amax=am)
+        res.append((q, am))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0].cpu(), res[1][0].cpu()) and torch.equal(res[0][1].cpu(), res[1][1].cpu())
