@@ -56,8 +56,10 @@ FP8_FFN2 = os.environ.get("SMER_FP8_FFN2", "1") == "1"
 FP8_EMBED = os.environ.get("SMER_FP8_EMBED", "0") == "1"
 # SMER_FP8_H8=1: once FFN1's e4m3 copy feeds FFN2 (its site has a scale
 # history), FFN1 writes that copy alone, and the FFN2 dgrad takes its ReLU /
-# dropout gate from the copy (smer_gemm_fp8_gate8): no bf16 [tokens, F]
-# activation is written or read back.  Needs the streamed e4m3-copy epilogue.
+# dropout gate from the copy (smer_gemm_fp8_gate8) and writes only dh's e4m3
+# copy when FFN1's weight gradient and dgrad both read it: no bf16 [tokens, F]
+# tensor is written or read back (C4 79.43 -> 78.17 ms).  Needs the streamed
+# e4m3-copy epilogue.
 FP8_H8 = (os.environ.get("SMER_FP8_H8", "1") == "1"
           and os.environ.get("SMER_FP8_Q8_FAST", "1") != "0")
 
@@ -529,14 +531,14 @@ class Engine:
                                                        accumulate=kw.get("accumulate", True), ws=ws,
                                                        max_wg=cap):
                 return
-            if x is None:
+            if x is None or dy is None:
                 raise RuntimeError("engine: fp8 weight gradient declined with no bf16 input")
             ops.linear_wgrad(dy, x, gw, ws=ws, max_wg=cap, **kw)
         if side is None:
             run(None, 0)
             return
         stream, ws = side
-        stream.wait_stream(torch.cuda.current_stream(dy.device))
+        stream.wait_stream(torch.cuda.current_stream(side[1].device))
         with torch.cuda.stream(stream):
             run(ws, _WGRAD_SIDE_CAP)
             if ops.CK_LOG is not None:
@@ -546,9 +548,9 @@ class Engine:
                 ops.ck("S:x", x)
         # temporaries freed on the main stream must not be reused before the
         # side stream has read them
-        dy.record_stream(stream)
-        if x is not None:
-            x.record_stream(stream)
+        for t in (dy, x):
+            if t is not None:
+                t.record_stream(stream)
         if q8 is not None:
             q8[0].record_stream(stream)
             q8[2].record_stream(stream)
@@ -627,14 +629,17 @@ class Engine:
             return (views[0], views[1], views[2], f8.qs_of(si), f8.amax_of(si)), \
                 ((buf, si) if site in f8.bwd_ready else None)
 
-        def dgrad(gq, g, wname, w, q_site=None, **epi):
+        def dgrad(gq, g, wname, w, q_site=None, q_only=False, **epi):
             """g @ w; on the fp8 MFMA (e4m3(g) . e4m3(w^T)^T) when g has a usable
-            e4m3 copy gq.  q_site: also the e4m3 copy of the output."""
-            M = g.shape[0]
+            e4m3 copy gq (g may then be None: only the copy exists).  q_site:
+            also the e4m3 copy of the output; q_only: only that copy once it is
+            usable (the bf16 output is then None, FP8_H8)."""
+            M = (g if g is not None else gq[0]).shape[0]
             if gq is not None:
                 wt = f8.weight_t(wname)
                 if wt is not None and eligible(M, w.shape[1], w.shape[0]):
-                    out = torch.empty(M, w.shape[1], dtype=dt, device=dev)
+                    out = None if (q_only and q_site is not None and q_site in f8.bwd_ready) else \
+                        torch.empty(M, w.shape[1], dtype=dt, device=dev)
                     if q_site is None:
                         if ops.gemm_fp8_ex(gq[0], f8.inv_of(gq[1]), wt[0], wt[1], out, **epi):
                             return out, None
@@ -646,6 +651,8 @@ class Engine:
                             f8.record_bwd(q_site)
                             return out, ((q, si) if q_site in f8.bwd_ready else None)
             # bf16 (also whenever the fp8 kernel declined the shape: nothing launched)
+            if g is None:
+                raise RuntimeError("engine: %s dgrad has only an e4m3 input but did not run fp8" % wname)
             return ops.linear_dgrad(g, w, **epi), None
 
         # vocab head
@@ -661,22 +668,27 @@ class Engine:
             if f8w is not None and dyq is not None and xq is not None:
                 kw["q8"] = (dyq[0], f8w.inv_of(dyq[1]), xq[0], f8w.inv_of(xq[1]))
             wg_(dy_, x_, gw, **kw)
-        def ffn2_bwd(dyq, dyd, name, w2, GL, h, hq, q_site):
+        def ffn2_bwd(dyq, dyd, name, w2, GL, h, hq, q_site, xq1, name1):
             """FFN2's weight gradient and gated dgrad (returns dh, its e4m3
             copy).  h None: FFN1 kept only its e4m3 copy hq (FP8_H8); the gate
             then comes from the copy (smer_gemm_fp8_gate8), and bf16 values
-            are rebuilt from it only where a bf16 fallback needs them."""
+            are rebuilt from it only where a bf16 fallback needs them.  dh
+            itself is written only as its e4m3 copy when both of its
+            consumers (FFN1's weight gradient with FFN1's input copy xq1, and
+            FFN1's dgrad, weight name1) will read that copy."""
             gs = ops.drop_scale(p_tr)
+            q_only = (FP8_H8 and f8 is not None and f8w is not None and xq1 is not None
+                      and f8.weight_t(name1) is not None and eligible(dyd.shape[0], w2.shape[0], w2.shape[1]))
             if h is None and not (f8 is not None and f8w is not None and dyq is not None
                                   and f8.weight_t(name) is not None):
                 h = self._deq8(hq, ctx.f8)
             wg(dyd, h, GL.l2_w, dyq, hq, db=GL.l2_b)
             if h is not None:
-                return dgrad(dyq, dyd, name, w2, q_site=q_site, gate=h, gate_scale=gs)
+                return dgrad(dyq, dyd, name, w2, q_site=q_site, q_only=q_only, gate=h, gate_scale=gs)
             wt = f8.weight_t(name)
             si = f8.site(q_site)
             M, N = dyd.shape[0], w2.shape[1]
-            out = torch.empty(M, N, dtype=dt, device=dev)
+            out = None if (q_only and q_site in f8.bwd_ready) else torch.empty(M, N, dtype=dt, device=dev)
             q = torch.empty(M, N, dtype=torch.uint8, device=dev)
             if not ops.gemm_fp8_gate8(dyq[0], f8.inv_of(dyq[1]), wt[0], wt[1], hq[0], gs, out, q,
                                       f8.qs_of(si), f8.amax_of(si)):
@@ -715,7 +727,8 @@ class Engine:
             dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
             dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
             ck("M:dec%d.dy3" % i, dy3d)
-            dh, dhq = ffn2_bwd(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, GL, h, hq, "b.dec%d.dh" % i)
+            dh, dhq = ffn2_bwd(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, GL, h, hq, "b.dec%d.dh" % i, x2q,
+                               "dec%d.l1" % i)
             ck("M:dec%d.dh" % i, dh)
             wg(dh, x2, GL.l1_w, dhq, x2q, db=GL.l1_b)
             dx2, _ = dgrad(dhq, dh, "dec%d.l1" % i, L.l1_w, residual=dy3)
@@ -796,7 +809,8 @@ class Engine:
             dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
             ck("M:enc%d.dy2" % i, dy2d)
-            dh, dhq = ffn2_bwd(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, GL, h, hq, "b.enc%d.dh" % i)
+            dh, dhq = ffn2_bwd(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, GL, h, hq, "b.enc%d.dh" % i, x1q,
+                               "enc%d.l1" % i)
             ck("M:enc%d.dh" % i, dh)
             wg(dh, x1, GL.l1_w, dhq, x1q, db=GL.l1_b)
             dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)

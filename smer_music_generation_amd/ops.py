@@ -458,7 +458,8 @@ def gemm_fp8_ex(a8, a_inv, b8, b_inv, out, *, bias=None, residual=None, gate=Non
     """out[M,N] bf16 = a_inv*b_inv * a8 @ b8^T (+ bias) (+ residual | ReLU gate:
     out = gate > 0 ? v * gate_scale : 0), optionally with the e4m3 copy of out
     (q8 = e4m3(out * qs), max|out| folded into amax).  The fp8 backward's
-    dgrad products.  Returns False (nothing launched) outside the tiling."""
+    dgrad products; out may be None beside q8 (the e4m3 copy alone, streamed
+    epilogue).  Returns False (nothing launched) outside the tiling."""
     M, K = a8.shape
     N = b8.shape[0]
     if M % 256 or N % 256 or K % 128:
@@ -470,7 +471,7 @@ def gemm_fp8_ex(a8, a_inv, b8, b_inv, out, *, bias=None, residual=None, gate=Non
         ev0.record()
     call("smer_gemm_fp8_ex", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
          _p(bias), 0, _p(residual), _ld(residual) if residual is not None else 0, _p(gate),
-         _ld(gate) if gate is not None else 0, float(gate_scale), 0.0, 0, _p(out), _ld(out), _p(q8),
+         _ld(gate) if gate is not None else 0, float(gate_scale), 0.0, 0, _p(out), _ld(out) if out is not None else 0, _p(q8),
          _ld(q8) if q8 is not None else 0, _p(qs), _p(amax), _stream())
     if timer is not None:
         ev1.record()
@@ -541,7 +542,8 @@ def gemm_fp8_gate8(a8, a_inv, b8, b_inv, gate8, gate_scale, out, q8, qs, amax):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
     call("smer_gemm_fp8_gate8", M, N, K, _p(a8), _ld(a8), _p(b8), _ld(b8), _p(a_inv), _p(b_inv),
-         _p(gate8), _ld(gate8), float(gate_scale), _p(out), _ld(out), _p(q8), _ld(q8), _p(qs), _p(amax),
+         _p(gate8), _ld(gate8), float(gate_scale), _p(out), _ld(out) if out is not None else 0, _p(q8), _ld(q8),
+         _p(qs), _p(amax),
          _stream())
     if timer is not None:
         ev1.record()

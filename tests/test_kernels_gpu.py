@@ -1514,6 +1514,16 @@ def test_fp8_e4m3_gate_and_copy_only_output():
     for x, y in zip(outs[0], outs[1]):
         assert torch.equal(x.cpu(), y.cpu())
     assert int((outs[1][0] == 0).sum()) > M * N // 5  # the gate closed somewhere
+    # both gated forms with a null C: the same e4m3 copy and amax alone
+    for use8 in (False, True):
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        am = torch.zeros(1, device=dev, dtype=torch.int32)
+        if use8:
+            assert O.gemm_fp8_gate8(a8, inv, b8, inv, g8, 1.25, None, q, qs, am)
+        else:
+            assert O.gemm_fp8_ex(a8, inv, b8, inv, None, gate=g_bf, gate_scale=1.25, q8=q, qs=qs, amax=am)
+        torch.cuda.synchronize()
+        assert torch.equal(q.cpu(), outs[1][1].cpu()) and torch.equal(am.cpu(), outs[1][2].cpu())
     # FFN1 with and without its bf16 output
     bias = torch.randn(N, generator=g).to(dev)
     res = []
