@@ -475,8 +475,10 @@ int smer_fp8_scales(int n, const unsigned* amax_prev, float* qs, float* inv, uns
  * smer_gemm_fp8_ex: smer_gemm_fp8_q plus a ReLU gate (C = gv > 0 ? v *
  * gate_scale : 0, exclusive with residual) for the FFN2 dgrad.
  * smer_layernorm_bwd_fp8: smer_layernorm_bwd (bf16) plus the e4m3 copy
- * q8 = e4m3(g * *qs) of the gradient that feeds the next dgrad (dx_drop when
- * given, else dx), max|g| folded into *amax; partials_only != 0 writes the
+ * q8 = e4m3(g * *qs) of the gradient that feeds the next dgrad (the dropped
+ * gradient when drop_p > 0, else dx; with drop_p > 0 and dx_drop null that
+ * gradient is written only as its copy), max|g| folded into *amax;
+ * partials_only != 0 writes the
  * dgamma / dbeta partials only (smer_layernorm_param_reduce later). */
 int smer_fp8_quantize_segments_t(int nseg, const int64_t* seg, unsigned* amax_ws, float* inv_scale,
                                  int blocks_per_seg, smer_stream_t stream);

@@ -353,9 +353,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const void* _
 #pragma unroll
           for (int i = 0; i < 8; ++i) o[i] = rs[u] * (gd[u][c][i] - s1[u] - xh[u][c][i] * s2[u]);
           Vec8<T>::store(dx + (long)row * lddx + ch * 8, o);
-          if (dxd) {
+          if (dxd || (Q8 && thr)) {  // (Q8 without dxd: the dropped values' e4m3 copy alone)
             if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)(ch * 8), o);
-            Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
+            if (dxd) Vec8<T>::store(dxd + (long)row * ldxd + ch * 8, o);
           }
           if constexpr (Q8) {  // e4m3 copy of the stored (T-rounded) values
             float r[8];
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
 #pragma unroll
       for (int i = 0; i < 4; ++i) wt[i] = (bf16)o[8 + i];
       if (tok) *reinterpret_cast<bf16x4*>(dx + (long)row * lddx + ct) = wt;
-      if (dxd) {
+      if (dxd || (Q8 && thr)) {  // (Q8 without dxd: the dropped values' e4m3 copy alone)
         float od[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) od[i] = o[i];
@@ -745,7 +745,7 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
         if (thr) smer_drop8(rowkey, thr, dscale, (uint32_t)c0, od);
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = (bf16)od[i];
-        *reinterpret_cast<bf16x8*>(dxd + (long)row * ldxd + c0) = w;
+        if (dxd) *reinterpret_cast<bf16x8*>(dxd + (long)row * ldxd + c0) = w;
         if (tok) {
           float ot[4] = {o[8], o[9], o[10], o[11]};
           if (thr) {
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256) void ln_bwd_t4_kernel(int M, int N, const bf16
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) wt[i] = (bf16)ot[i];
-          *reinterpret_cast<bf16x4*>(dxd + (long)row * ldxd + ct) = wt;
+          if (dxd) *reinterpret_cast<bf16x4*>(dxd + (long)row * ldxd + ct) = wt;
         }
       }
       if constexpr (Q8) {  // e4m3 copy of the last stored (bf16) values: w / wt

@@ -677,8 +677,9 @@ class Engine:
             consumers (FFN1's weight gradient with FFN1's input copy xq1, and
             FFN1's dgrad, weight name1) will read that copy."""
             gs = ops.drop_scale(p_tr)
+            Mr = (dyd if dyd is not None else dyq[0]).shape[0]
             q_only = (FP8_H8 and f8 is not None and f8w is not None and xq1 is not None
-                      and f8.weight_t(name1) is not None and eligible(dyd.shape[0], w2.shape[0], w2.shape[1]))
+                      and f8.weight_t(name1) is not None and eligible(Mr, w2.shape[0], w2.shape[1]))
             if h is None and not (f8 is not None and f8w is not None and dyq is not None
                                   and f8.weight_t(name) is not None):
                 h = self._deq8(hq, ctx.f8)
@@ -687,7 +688,7 @@ class Engine:
                 return dgrad(dyq, dyd, name, w2, q_site=q_site, q_only=q_only, gate=h, gate_scale=gs)
             wt = f8.weight_t(name)
             si = f8.site(q_site)
-            M, N = dyd.shape[0], w2.shape[1]
+            M, N = Mr, w2.shape[1]
             out = None if (q_only and q_site in f8.bwd_ready) else torch.empty(M, N, dtype=dt, device=dev)
             q = torch.empty(M, N, dtype=torch.uint8, device=dev)
             if not ops.gemm_fp8_gate8(dyq[0], f8.inv_of(dyq[1]), wt[0], wt[1], hq[0], gs, out, q,
@@ -695,6 +696,22 @@ class Engine:
                 raise RuntimeError("engine: %s e4m3-gated dgrad declined its shape" % name)
             f8.record_bwd(q_site)
             return out, ((q, si) if q_site in f8.bwd_ready else None)
+
+        def q_only_grad(xq_, name, w, site):
+            """Whether the output gradient of Linear `name` (weight w [N, K],
+            input copy xq_) may exist only as its e4m3 copy: its weight
+            gradient and dgrad both read that copy (the LayerNorm backward's
+            dropped gradient then is not written in bf16, FP8_H8)."""
+            M = ctx.B * (ctx.S if name.startswith("enc") else ctx.T)
+            return (FP8_H8 and p_tr > 0 and f8 is not None and f8w is not None and xq_ is not None
+                    and site in f8.bwd_ready and f8.weight_t(name) is not None
+                    and eligible(M, w.shape[1], w.shape[0]) and w.shape[0] % 256 == 0 and M % 64 == 0)
+
+        def dgrad_in(y_, xq_, name, w, site):
+            """The LayerNorm backward's dropped-gradient buffer (None: copy only)."""
+            if p_tr == 0:
+                return None
+            return None if q_only_grad(xq_, name, w, site) else torch.empty_like(y_)
 
         ops.ck("M:dlog", dlog_pad)
         wg(dlog_pad, ctx.dec_out, G.fc_w, M=V, db=G.fc_b)
@@ -724,7 +741,7 @@ class Engine:
             yq_in, oq, x1q, ocq, x2q, hq = ctx.dec_q[i]
             # FFN block: x3 = LN3(x2 + drop(W2 drop(relu(W1 x2))))
             dy3 = torch.empty_like(y3)
-            dy3d = torch.empty_like(y3) if p_tr > 0 else dy3
+            dy3d = dgrad_in(y3, hq, "dec%d.l2" % i, L.l2_w, "b.dec%d.ln3" % i) if p_tr > 0 else dy3
             dy3q = ln_bwd(dy, y3, m3, r3, L.n3, dy3, dy3d, sd(_site("dec", i, 5)), GL.n3, "b.dec%d.ln3" % i)
             ck("M:dec%d.dy3" % i, dy3d)
             dh, dhq = ffn2_bwd(dy3q, dy3d, "dec%d.l2" % i, L.l2_w, GL, h, hq, "b.dec%d.dh" % i, x2q,
@@ -735,7 +752,7 @@ class Engine:
             ck("M:dec%d.dx2" % i, dx2)
             # cross-attention block: x2 = LN2(x1 + drop(Wo attn(q(x1), kv(mem))))
             dy2 = torch.empty_like(y2)
-            dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
+            dy2d = dgrad_in(y2, ocq, "dec%d.cao" % i, L.ca_ow, "b.dec%d.ln2" % i) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx2, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("dec", i, 3)), GL.n2, "b.dec%d.ln2" % i)
             ck("M:dec%d.dy2" % i, dy2d)
             wg(dy2d, oc, GL.ca_ow, dy2q, ocq, db=GL.ca_ob)
@@ -766,7 +783,7 @@ class Engine:
             ck("M:dec%d.dx1" % i, dx1)
             # self-attention block
             dy1 = torch.empty_like(y1)
-            dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
+            dy1d = dgrad_in(y1, oq, "dec%d.sao" % i, L.sa_ow, "b.dec%d.ln1" % i) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("dec", i, 1)), GL.n1, "b.dec%d.ln1" % i)
             ck("M:dec%d.dy1" % i, dy1d)
             wg(dy1d, o, GL.sa_ow, dy1q, oq, db=GL.sa_ob)
@@ -806,7 +823,7 @@ class Engine:
             (x_in, qkv, o, lse, y1, m1, r1, x1, h, y2, m2, r2) = ctx.enc[i]
             xq_in, oq, x1q, hq = ctx.enc_q[i]
             dy2 = torch.empty_like(y2)
-            dy2d = torch.empty_like(y2) if p_tr > 0 else dy2
+            dy2d = dgrad_in(y2, hq, "enc%d.l2" % i, L.l2_w, "b.enc%d.ln2" % i) if p_tr > 0 else dy2
             dy2q = ln_bwd(dx, y2, m2, r2, L.n2, dy2, dy2d, sd(_site("enc", i, 3)), GL.n2, "b.enc%d.ln2" % i)
             ck("M:enc%d.dy2" % i, dy2d)
             dh, dhq = ffn2_bwd(dy2q, dy2d, "enc%d.l2" % i, L.l2_w, GL, h, hq, "b.enc%d.dh" % i, x1q,
@@ -816,7 +833,7 @@ class Engine:
             dx1, _ = dgrad(dhq, dh, "enc%d.l1" % i, L.l1_w, residual=dy2)
             ck("M:enc%d.dx1" % i, dx1)
             dy1 = torch.empty_like(y1)
-            dy1d = torch.empty_like(y1) if p_tr > 0 else dy1
+            dy1d = dgrad_in(y1, oq, "enc%d.out" % i, L.out_w, "b.enc%d.ln1" % i) if p_tr > 0 else dy1
             dy1q = ln_bwd(dx1, y1, m1, r1, L.n1, dy1, dy1d, sd(_site("enc", i, 1)), GL.n1, "b.enc%d.ln1" % i)
             ck("M:enc%d.dy1" % i, dy1d)
             wg(dy1d, o, GL.out_w, dy1q, oq, db=GL.out_b)

@@ -655,7 +655,9 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, dx, *, dx_drop=None, drop_p=0.0, see
     """param_stream: run the dgamma / dbeta column reduction on that stream
     (after this stream's LayerNorm kernel), off the dgrad chain.  q8 (bf16
     only): also the e4m3 copy e4m3(g * qs) of the gradient g that feeds the
-    next dgrad (dx_drop when given, else dx), max|g| folded into amax."""
+    next dgrad (the dropped gradient when drop_p > 0, else dx), max|g| folded
+    into amax; with q8, drop_p > 0 and no dx_drop that gradient exists only
+    as its copy."""
     lib = load()
     M, N = x.shape
     nbytes = lib.smer_layernorm_bwd_workspace(M, N) if (dgamma is not None or dbeta is not None) else 0

@@ -1536,3 +1536,36 @@ def test_fp8_e4m3_gate_and_copy_only_output():
         res.append((q, am))
     torch.cuda.synchronize()
     assert torch.equal(res[0][0].cpu(), res[1][0].cpu()) and torch.equal(res[0][1].cpu(), res[1][1].cpu())
+
+
+@pytest.mark.parametrize("N", [768, 512])
+def test_layernorm_bwd_fp8_copy_only_dropped_gradient(N):
+    """smer_layernorm_bwd_fp8 with dropout and no dx_drop buffer: the same dx,
+    e4m3 copy of the dropped gradient and amax as with the buffer (N = 768 runs
+    the 12-column kernel, 512 the generic one)."""
+    O = ops()
+    M = 1024
+    g = torch.Generator(device="cpu").manual_seed(9)
+    x = torch.randn(M, N, generator=g).to(dev).to(torch.bfloat16)
+    dy = torch.randn(M, N, generator=g).to(dev).to(torch.bfloat16)
+    gamma = (torch.rand(N, generator=g) + 0.5).to(dev)
+    beta = torch.zeros(N, device=dev)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    O.layernorm(x, gamma, beta, y, mean, rstd)
+    qs = torch.tensor([40.0], device=dev)
+    res = []
+    for with_buf in (True, False):
+        dx = torch.empty_like(x)
+        dxd = torch.empty_like(x) if with_buf else None
+        q = torch.empty(M, N, device=dev, dtype=torch.uint8)
+        am = torch.zeros(1, device=dev, dtype=torch.int32)
+        O.layernorm_bwd(dy, x, mean, rstd, gamma, dx, dx_drop=dxd, drop_p=0.1, seed=11, q8=q, qs=qs, amax=am)
+        res.append((dx, q, am, dxd))
+    torch.cuda.synchronize()
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(a.cpu(), b.cpu())
+    want = (res[0][3].float().cpu() * 40.0).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(res[1][1].cpu(), want)
+    assert not torch.equal(res[0][0].cpu(), res[0][3].cpu())  # dropout did act
