@@ -732,8 +732,9 @@ def main():
                                          "Q and K/V; e4m3 dgrads: FFN2, FFN1, out-projections, "
                                          "QKV, cross Q, memory; e4m3 weight + bias gradients: "
                                          "the same Linears; delayed per-tensor scaling; "
-                                         "attention, the first layers' QKV and the vocab head "
-                                         "bf16)",
+                                         "FFN1's output, dh and the dropped LayerNorm "
+                                         "gradients stored in e4m3 only; attention, the first "
+                                         "layers' QKV and the vocab head bf16)",
                                 "value": round(c4["tokens_per_s"], 1),
                                 "ms_per_step": round(c4["ms_per_step"], 2),
                                 "step_tflops_per_gpu": round(c4["step_tflops_per_gpu"], 1),
