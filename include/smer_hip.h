@@ -178,7 +178,8 @@ int smer_attn_bwd(int dtype, int B, int H, int Lq, int Lk, int D,
  * (dq8, nullable) and of dK / dV (dk8 and dv8 together, nullable) beside the
  * bf16 gradients, folding max|g| into *amax (float bits, atomicMax): the fp8
  * input of the QKV / cross-Q dgrads in the C4 fp8 step (transformer.py:389,
- * 459 differentiated by train.py:783).  Copies 4-B aligned, strides % 4. */
+ * 459 differentiated by train.py:783).  Copies 4-B aligned, strides % 4.
+ * A gradient with a copy may be null itself (dk with dv): the copy alone. */
 int smer_attn_bwd_fp8(int B, int H, int Lq, int Lk, int D, const void* q, long ldq,
                       const void* k, long ldk, const void* v, long ldv, const void* o, long ldo,
                       const void* dout, long lddo, const float* lse, const uint8_t* kpm,

@@ -754,8 +754,10 @@ __global__ __launch_bounds__(256, KG == 2 ? 2 : 3) void attn_bwd_dkdv_bf16(
         wk[r] = (bf16)(kvalid ? adk[gk][dt][r] * scale : 0.f);
         wv[r] = (bf16)(kvalid ? adv[gk][dt][r] * (DROP ? drop_scale : 1.f) : 0.f);
       }
-      *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
-      *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
+      if (dk) {  // (null: the e4m3 copies alone)
+        *reinterpret_cast<bf16x4*>(dkr + dt * 16 + 4 * g) = wk;
+        *reinterpret_cast<bf16x4*>(dvr + dt * 16 + 4 * g) = wv;
+      }
       if (w8) {  // e4m3 copies of the stored (bf16-rounded) values
         float fk[4], fv[4];
 #pragma unroll
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(256, QG == 2 ? 2 : 3) void attn_bwd_dq_bf16(
       bf16x4 w;
 #pragma unroll
       for (int r = 0; r < 4; ++r) w[r] = (bf16)(adq[gq][dt][r] * scale);
-      *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;
+      if (dq) *reinterpret_cast<bf16x4*>(dqr + dt * 16 + 4 * g) = w;  // (null: the e4m3 copy alone)
       if (w8) {  // e4m3 copy of the stored (bf16-rounded) values
         float f[4];
 #pragma unroll
@@ -2075,7 +2077,9 @@ static int attn_bwd_impl(int dtype, int B, int H, int Lq, int Lk, int D, const v
                          void* dv, long lddv, void* workspace, size_t ws_bytes,
                          const void* drop_mask, const AttnQ8& q8, smer_stream_t stream) {
   SMER_REQUIRE(B > 0 && H > 0 && Lq > 0 && Lk > 0 && D > 0, "smer_attn_bwd: bad sizes");
-  SMER_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv, "smer_attn_bwd: null pointer");
+  // (bf16 with e4m3 copies: dq, or dk with dv, may be null beside their copies)
+  SMER_REQUIRE(q && k && v && o && dout && lse && (dq || q8.dq) && (dk || q8.dk) && !dk == !dv,
+               "smer_attn_bwd: null pointer");
   SMER_REQUIRE(workspace && ws_bytes >= smer_attn_bwd_workspace(dtype, B, H, Lq, Lk),
                "smer_attn_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;

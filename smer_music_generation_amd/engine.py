@@ -58,8 +58,9 @@ FP8_EMBED = os.environ.get("SMER_FP8_EMBED", "0") == "1"
 # history), FFN1 writes that copy alone, and the FFN2 dgrad takes its ReLU /
 # dropout gate from the copy (smer_gemm_fp8_gate8) and writes only dh's e4m3
 # copy when FFN1's weight gradient and dgrad both read it: no bf16 [tokens, F]
-# tensor is written or read back (C4 79.43 -> 78.17 ms).  Needs the streamed
-# e4m3-copy epilogue.
+# tensor is written or read back (C4 79.43 -> 78.17 ms).  Likewise the
+# LayerNorm backward's dropped gradients and the attention backward's dQKV
+# (all four: C4 79.06 -> 76.86 ms).  Needs the streamed e4m3-copy epilogue.
 FP8_H8 = (os.environ.get("SMER_FP8_H8", "1") == "1"
           and os.environ.get("SMER_FP8_Q8_FAST", "1") != "0")
 
@@ -697,13 +698,14 @@ class Engine:
             f8.record_bwd(q_site)
             return out, ((q, si) if q_site in f8.bwd_ready else None)
 
-        def q_only_grad(xq_, name, w, site):
+        def q_only_grad(xq_, name, w, site, dropped=True):
             """Whether the output gradient of Linear `name` (weight w [N, K],
             input copy xq_) may exist only as its e4m3 copy: its weight
             gradient and dgrad both read that copy (the LayerNorm backward's
-            dropped gradient then is not written in bf16, FP8_H8)."""
+            dropped gradient, dropped=True, or the attention backward's dQKV
+            then is not written in bf16, FP8_H8)."""
             M = ctx.B * (ctx.S if name.startswith("enc") else ctx.T)
-            return (FP8_H8 and p_tr > 0 and f8 is not None and f8w is not None and xq_ is not None
+            return (FP8_H8 and (p_tr > 0 or not dropped) and f8 is not None and f8w is not None and xq_ is not None
                     and site in f8.bwd_ready and f8.weight_t(name) is not None
                     and eligible(M, w.shape[1], w.shape[0]) and w.shape[0] % 256 == 0 and M % 64 == 0)
 
@@ -789,10 +791,14 @@ class Engine:
             wg(dy1d, o, GL.sa_ow, dy1q, oq, db=GL.sa_ob)
             do, _ = dgrad(dy1q, dy1d, "dec%d.sao" % i, L.sa_ow)
             ck("M:dec%d.do" % i, do)
-            dqkv = torch.empty(Mt, 3 * d, dtype=dt, device=dev)
             q8s, dqkvq = attn_q8((Mt, 3 * d), "b.dec%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
-            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
-                         dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=T, Lk=T, D=D,
+            dqkv = None if (q8s is not None and q_only_grad(yq_in, "dec%d.sa" % i, L.sa_w, "b.dec%d.dqkv" % i,
+                                                            dropped=False)) else \
+                torch.empty(Mt, 3 * d, dtype=dt, device=dev)
+            dq_, dk_, dv_ = (None, None, None) if dqkv is None else \
+                (dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:])
+            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dq_,
+                         dk_, dv_, B=B, H=H, Lq=T, Lk=T, D=D,
                          kpm=ctx.tkpm, causal=True, scale=scale, drop_p=p_tr,
                          seed=sd(_site("dec", i, 0)), drop_mask=ctx.masks.get(("dec", i)), q8=q8s)
             ck("M:dec%d.dqkv" % i, dqkv)
@@ -839,10 +845,14 @@ class Engine:
             wg(dy1d, o, GL.out_w, dy1q, oq, db=GL.out_b)
             do, _ = dgrad(dy1q, dy1d, "enc%d.out" % i, L.out_w)
             ck("M:enc%d.do" % i, do)
-            dqkv = torch.empty(Ms, 3 * d, dtype=dt, device=dev)
             q8s, dqkvq = attn_q8((Ms, 3 * d), "b.enc%d.dqkv" % i, [(0, d), (d, 2 * d), (2 * d, 3 * d)])
-            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dqkv[:, :d],
-                         dqkv[:, d:2 * d], dqkv[:, 2 * d:], B=B, H=H, Lq=S, Lk=S, D=D,
+            dqkv = None if (q8s is not None and q_only_grad(xq_in, "enc%d.in" % i, L.in_w, "b.enc%d.dqkv" % i,
+                                                            dropped=False)) else \
+                torch.empty(Ms, 3 * d, dtype=dt, device=dev)
+            dq_, dk_, dv_ = (None, None, None) if dqkv is None else \
+                (dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:])
+            ops.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, dq_,
+                         dk_, dv_, B=B, H=H, Lq=S, Lk=S, D=D,
                          kpm=ctx.skpm, causal=False, scale=scale, drop_p=p_tr,
                          seed=sd(_site("enc", i, 0)), drop_mask=ctx.masks.get(("enc", i)), q8=q8s)
             ck("M:enc%d.dqkv" % i, dqkv)

@@ -290,7 +290,8 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, caus
              scale, drop_p=0.0, seed=0, drop_mask=None, q8=None):
     """q8 (bf16): (dq8, dk8, dv8, qs, amax) -- e4m3 copies of the gradients
     (uint8 views shaped like dq / dk / dv; dq8 or dk8 + dv8 may be None)
-    scaled by qs[0], max|g| folded into amax (smer_attn_bwd_fp8)."""
+    scaled by qs[0], max|g| folded into amax (smer_attn_bwd_fp8); a gradient
+    with a copy may then be None itself (dk with dv): the copy alone."""
     lib = load()
     dt = dtype_code(q.dtype)
     nbytes = lib.smer_attn_bwd_workspace(dt, B, H, Lq, Lk)
@@ -302,8 +303,8 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, kpm=None, caus
         ld8 = lambda t: _ld(t) if t is not None else 0  # noqa: E731
         call("smer_attn_bwd_fp8", B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v),
              _p(o), _ld(o), _p(do), _ld(do), _p(lse), _p(kpm), int(causal), float(scale),
-             float(drop_p), int(seed) & 0xFFFFFFFF, _p(dq), _ld(dq), _p(dk), _ld(dk), _p(dv),
-             _ld(dv), _p(ws), nbytes, _p(drop_mask), _p(dq8), ld8(dq8), _p(dk8), ld8(dk8),
+             float(drop_p), int(seed) & 0xFFFFFFFF, _p(dq), ld8(dq), _p(dk), ld8(dk), _p(dv),
+             ld8(dv), _p(ws), nbytes, _p(drop_mask), _p(dq8), ld8(dq8), _p(dk8), ld8(dk8),
              _p(dv8), ld8(dv8), _p(qs), _p(amax), _stream())
         return
     call("smer_attn_bwd", dt, B, H, Lq, Lk, D, _p(q), _ld(q), _p(k), _ld(k), _p(v), _ld(v),

@@ -590,6 +590,14 @@ def test_attention_bwd_e4m3_copies(kg2):
         assert torch.equal(q8[:, j * hd:(j + 1) * hd], want)
     m = max(t.float().abs().max().item() for t in ref)
     assert amax.view(torch.float32).item() == m
+    # no bf16 gradients (the fp8 step's dQKV when both its consumers read the
+    # copies): the same copies and amax alone
+    q8b = torch.zeros_like(q8)
+    amb = torch.zeros(1, dtype=torch.int32, device=dev)
+    O.attn_bwd(q, k, v, o, do, lse, None, None, None, B=B, H=H, Lq=L, Lk=L, D=D, kpm=kpm, scale=0.125,
+               drop_p=0.1, seed=5, q8=(q8b[:, :hd], q8b[:, hd:2 * hd], q8b[:, 2 * hd:], qs, amb))
+    torch.cuda.synchronize()
+    assert torch.equal(q8b, q8) and torch.equal(amb, amax)
 
 
 @pytest.mark.parametrize("dtype,B,H,L,causal", [(torch.bfloat16, 2, 2, 96, True),
