@@ -59,8 +59,9 @@ FP8_EMBED = os.environ.get("SMER_FP8_EMBED", "0") == "1"
 # dropout gate from the copy (smer_gemm_fp8_gate8) and writes only dh's e4m3
 # copy when FFN1's weight gradient and dgrad both read it: no bf16 [tokens, F]
 # tensor is written or read back (C4 79.43 -> 78.17 ms).  Likewise the
-# LayerNorm backward's dropped gradients and the attention backward's dQKV
-# (all four: C4 79.06 -> 76.86 ms).  Needs the streamed e4m3-copy epilogue.
+# LayerNorm backward's dropped gradients and the attention backward's dQKV,
+# cross dQ and memory dK|dV (all: C4 78.70 -> 76.12 ms).  Needs the streamed
+# e4m3-copy epilogue.
 FP8_H8 = (os.environ.get("SMER_FP8_H8", "1") == "1"
           and os.environ.get("SMER_FP8_Q8_FAST", "1") != "0")
 
@@ -730,12 +731,17 @@ class Engine:
             self._hook(side, hook, "head")
         # every layer's dK|dV of the memory lands in one [Ms, L*2d] buffer:
         # one dgrad GEMM (K = L*2d) after the decoder loop gives dmemory
-        dkvc_all = torch.empty(Ms, self.n_dec * 2 * d, dtype=dt, device=dev)
         # fp8: one e4m3 copy of it (and of each layer's cross dQ) under one
-        # scale site, so the memory dgrad runs on the fp8 MFMA as well
+        # scale site, so the memory dgrad runs on the fp8 MFMA as well; with
+        # FP8_H8 and every consumer on the copy (each layer's K/V weight
+        # gradient, the memory dgrad) the bf16 buffer is not written at all
         cross8 = None
         if f8 is not None and FP8_ATTN_DGRAD and self.n_dec:
             cross8 = (f8.site("b.cross"), torch.empty(Ms, self.n_dec * 2 * d, dtype=torch.uint8, device=dev))
+        kv_q_only = (cross8 is not None and FP8_H8 and f8w is not None and "b.cross" in f8.bwd_ready
+                     and ctx.memq is not None and f8.weight_t("ckv") is not None
+                     and eligible(Ms, d, self.n_dec * 2 * d) and (2 * d) % 256 == 0 and Ms % 64 == 0)
+        dkvc_all = None if kv_q_only else torch.empty(Ms, self.n_dec * 2 * d, dtype=dt, device=dev)
         for i in reversed(range(self.n_dec)):
             L, GL = W.dec[i], G.dec[i]
             (y_in, qkv, o, lse, y1, m1, r1, x1, qc, kvc, oc, lsec, y2, m2, r2, x2, h, y3, m3,
@@ -760,8 +766,10 @@ class Engine:
             wg(dy2d, oc, GL.ca_ow, dy2q, ocq, db=GL.ca_ob)
             doc, _ = dgrad(dy2q, dy2d, "dec%d.cao" % i, L.ca_ow)
             ck("M:dec%d.doc" % i, doc)
-            dqc = torch.empty(Mt, d, dtype=dt, device=dev)
-            dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d]
+            dqc = None if (cross8 is not None and q_only_grad(x1q, "dec%d.cq" % i, L.cq_w, "b.cross",
+                                                              dropped=False)) else \
+                torch.empty(Mt, d, dtype=dt, device=dev)
+            dkvc = dkvc_all[:, i * 2 * d:(i + 1) * 2 * d] if dkvc_all is not None else None
             q8c, dqcq = None, None
             if cross8 is not None:
                 si, dkvc8 = cross8
@@ -770,7 +778,8 @@ class Engine:
                        f8.qs_of(si), f8.amax_of(si))
                 f8.record_bwd("b.cross")
                 dqcq = (dqc8, si) if "b.cross" in f8.bwd_ready else None
-            ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc, dkvc[:, :d], dkvc[:, d:],
+            ops.attn_bwd(qc, kvc[:, :d], kvc[:, d:], oc, doc, lsec, dqc,
+                         dkvc[:, :d] if dkvc is not None else None, dkvc[:, d:] if dkvc is not None else None,
                          B=B, H=H, Lq=T, Lk=S, D=D, kpm=ctx.mkpm, causal=False, scale=scale,
                          drop_p=p_tr, seed=sd(_site("dec", i, 2)), drop_mask=ctx.masks.get(("cross", i)),
                          q8=q8c)
@@ -809,8 +818,8 @@ class Engine:
                 self._hook(side, hook, "dec%d" % i)
         d_tgt = dy
         if self.n_dec:
-            if (cross8 is not None and "b.cross" in f8.bwd_ready and f8.weight_t("ckv") is not None
-                    and eligible(Ms, d, self.n_dec * 2 * d)):
+            if kv_q_only or (cross8 is not None and "b.cross" in f8.bwd_ready and f8.weight_t("ckv") is not None
+                             and eligible(Ms, d, self.n_dec * 2 * d)):
                 # bf16 output (the bf16 path sums into fp32): its rounding,
                 # unit roundoff 2^-9, is far below the e4m3 operands' 2^-4
                 dmem, _ = dgrad((cross8[1], cross8[0]), dkvc_all, "ckv", W.ckv_all)
