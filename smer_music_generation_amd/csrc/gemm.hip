@@ -754,25 +754,10 @@ constexpr int G2_LDS = G2_XA + 64 * G2 * 2;         // 160 KiB total
 
 // 64 rows x 256 bf16 columns of X (row-major, ld) -> LDS [64][512 B], by
 // LDS-DMA: wave w's instruction c fills 1 KiB = rows 2(4w+c), +1.
-// G8: 64 rows x 256 byte columns (an e4m3 gate) -> LDS [64][256 B]: wave w's
-// instruction c fills rows 4(2w+c) .. +3.
-__device__ __forceinline__ void g2_xload(char* dst, const void* Xv, long ld, int r0, int c0, int tid,
-                                         bool g8 = false) {
+__device__ __forceinline__ void g2_xload(char* dst, const bf16* X, long ld, int r0, int c0, int tid) {
   typedef __attribute__((address_space(1))) void gvoid;
   typedef __attribute__((address_space(3))) void lvoid;
   const int lane = tid & 63, wave = tid >> 6;
-  if (g8) {
-    const uint8_t* X8 = (const uint8_t*)Xv;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int chunk = wave * 2 + c;
-      const int row = chunk * 4 + (lane >> 4);
-      const uint8_t* src = X8 + (long)(r0 + row) * ld + c0 + (lane & 15) * 16;
-      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + chunk * 1024), 16, 0, 0);
-    }
-    return;
-  }
-  const bf16* X = (const bf16*)Xv;
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     const int chunk = wave * 4 + c;
@@ -780,6 +765,26 @@ __device__ __forceinline__ void g2_xload(char* dst, const void* Xv, long ld, int
     const bf16* src = X + (long)(r0 + row) * ld + c0 + (lane & 31) * 8;
     __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + chunk * 1024), 16, 0, 0);
   }
+}
+// 64 rows x 256 byte columns (an e4m3 gate) -> LDS [64][256 B]: wave w's
+// instruction c fills rows 4(2w+c) .. +3.
+__device__ __forceinline__ void g2_xload8(char* dst, const uint8_t* X, long ld, int r0, int c0, int tid) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int chunk = wave * 2 + c;
+    const int row = chunk * 4 + (lane >> 4);
+    const uint8_t* src = X + (long)(r0 + row) * ld + c0 + (lane & 15) * 16;
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + chunk * 1024), 16, 0, 0);
+  }
+}
+// X rows of one epilogue pass: bf16, or (G8) the bytes of an e4m3 gate
+template <bool G8>
+__device__ __forceinline__ void g2_xload_any(char* dst, const bf16* X, long ld, int r0, int c0, int tid) {
+  if constexpr (G8) g2_xload8(dst, (const uint8_t*)X, ld, r0, c0, tid);
+  else g2_xload(dst, X, ld, r0, c0, tid);
 }
 
 // LDS image of one operand stage: KC (row image): row r at r*128 B, 16-B
@@ -839,7 +844,7 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* buf, int rbase, int s, int
 template <bool Q8, bool G8 = false>
 __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (&acc)[8][4], char* smem,
                                                  int m0, int n0, int tid, const float (&bv)[8],
-                                                 const void* xsrc, long ldx, float& amax_acc) {
+                                                 const bf16* xsrc, long ldx, float& amax_acc) {
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int g = lane >> 4, c16 = lane & 15;
@@ -847,8 +852,7 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
   float* ep = reinterpret_cast<float*>(smem);
   float q8s = 1.f;
   if constexpr (Q8) q8s = *e.q8_scale;
-  constexpr bool g8 = G8;
-  if (xsrc) g2_xload(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid, g8);
+  if (xsrc) g2_xload_any<G8>(smem + G2_XB, xsrc, ldx, m0 + 64, n0, tid);
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
     if (wm == (pass >> 1)) {
@@ -867,7 +871,7 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
     if (xsrc) __syncthreads();
     else smer_lds_barrier();
     if (xsrc && pass >= 1 && pass < 3)
-      g2_xload(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid, g8);
+      g2_xload_any<G8>(smem + ((pass + 1) & 1 ? G2_XB : G2_XA), xsrc, ldx, m0 + 64 * (pass + 1), n0, tid);
     const char* xs = smem + ((pass & 1) ? G2_XB : G2_XA);
     const int ch = tid & 31;
     // Q8: one item at a time (unrolled, the four items' temporaries beside
@@ -888,7 +892,7 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
       }
       if (e.drop_thr)
         smer_drop8(smer_rowkey(e.seed, (uint32_t)grow), e.drop_thr, e.drop_scale, (uint32_t)gcol, v);
-      if (xsrc && g8) {
+      if constexpr (G8) {
         const uint2 gb = *reinterpret_cast<const uint2*>(xs + row * 256 + ch * 8);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -908,8 +912,11 @@ __device__ __forceinline__ void g2_fast_epilogue(const GemmEpi& e, const f32x4 (
       bf16x8 o;
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = (bf16)v[k];
-      if (!Q8 || e.C)  // (Q8: the e4m3 copy alone when C is null)
+      if constexpr (Q8) {  // (the e4m3 copy alone when C is null)
+        if (e.C) *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+      } else {
         *reinterpret_cast<bf16x8*>((bf16*)e.C + (long)grow * e.ldc + gcol) = o;
+      }
       if constexpr (Q8) {  // e4m3 copy of the stored (bf16-rounded) values
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = (float)o[k];
@@ -3633,7 +3640,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
   GemmEpi ee = e;
   ee.alpha = e.alpha * (*a_inv) * (*b_inv);  // dequantisation of both operands
   float amax_acc = 0.f;
-  const void* xsrc = e.residual ? e.residual : e.gate;  // streamed epilogue operand
+  const bf16* xsrc = (const bf16*)(e.residual ? e.residual : e.gate);  // streamed epilogue operand (G8: bytes)
   const long ldx = e.residual ? e.ldr : e.ldg;
   g2_start_skew(e.skew);
 
@@ -3664,7 +3671,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_fp8_kernel(int M, int N, int K
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // stage kt landed; stage kt-1 fully read
       // X rows of the first epilogue pass into slot A (beyond the stages)
-      if (FAST && xsrc && kt == nk / 2) g2_xload(smem + G2_XA, xsrc, ldx, m0, n0, tid, G8);
+      if (FAST && xsrc && kt == nk / 2) g2_xload_any<G8>(smem + G2_XA, xsrc, ldx, m0, n0, tid);
       if (kt + 1 < nk) {
         char* nb = smem + ((kt + 1) & 1) * G2_STAGE;
         f8_glds(nb, A, lda, M, m0, (kt + 1) * F8K, tid);
